@@ -1,0 +1,102 @@
+"""ctypes binding of libldpc5g.so (include/ldpc5g.h) plus device-buffer helpers.
+
+PyTorch-ROCm is used only for device memory and the current HIP stream; no torch ops run on
+the hot path.  There is no CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libldpc5g.so")
+
+F64, F32 = 0, 1
+FLOODING, LAYERED = 0, 1
+LLR_FULL = 1
+EBGN, EZC, ESIZE, EHIP = -1, -2, -3, -4
+
+# every symbol include/ldpc5g.h declares: name -> (restype, argtypes)
+_c = ctypes
+SIGNATURES = {
+    "ldpc5g_find_ils": (_c.c_int, [_c.c_int32]),
+    "ldpc5g_encode": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_int32, _c.c_int32,
+                                 _c.c_int64, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_decode_ms": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                    _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_double,
+                                    _c.c_double, _c.c_int32, _c.c_int32, _c.c_int64, _c.c_int64,
+                                    _c.c_void_p]),
+    "ldpc5g_decode_ms_mixed": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_int32,
+                                          _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                          _c.c_double, _c.c_double, _c.c_int32, _c.c_int32,
+                                          _c.c_void_p]),
+    "ldpc5g_last_error": (_c.c_char_p, []),
+    "ldpc5g_version": (_c.c_char_p, []),
+}
+
+
+class CbDesc(ctypes.Structure):
+    """ldpc5g_cb_desc_t"""
+    _fields_ = [("bgn", ctypes.c_int32), ("Zc", ctypes.c_int32),
+                ("llr_off", ctypes.c_int64), ("ck_off", ctypes.c_int64)]
+
+
+class LdpcLibError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libldpc5g.so (raises LdpcLibError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LdpcLibError(
+                f"{LIB_PATH} is missing: build it with `python -m python_5gtoolbox_amd.build` "
+                "(there is no CPU fallback for the LDPC hot path)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc):
+    """Map a negative return code to the reference's error behaviour (AssertionError for
+    argument errors, as its `assert` checks) or LdpcLibError for HIP failures."""
+    if rc == 0:
+        return
+    msg = lib().ldpc5g_last_error().decode()
+    if rc in (EBGN, EZC, ESIZE):
+        raise AssertionError(msg)
+    raise LdpcLibError(f"libldpc5g error {rc}: {msg}")
+
+
+_torch = None
+
+
+def torch():
+    global _torch
+    if _torch is None:
+        import torch as t
+        _torch = t
+    return _torch
+
+
+def require_gpu():
+    t = torch()
+    if not t.cuda.is_available():
+        raise LdpcLibError("no ROCm GPU visible: the LDPC engine runs only on the GPU "
+                           "(no CPU fallback)")
+    return t
+
+
+def stream_ptr(device=None):
+    t = torch()
+    return ctypes.c_void_p(t.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(tensor):
+    return ctypes.c_void_p(tensor.data_ptr())

@@ -1,0 +1,104 @@
+"""TS 38.212 §5.1 CRC attach / check — host-side mirror of py5gphy/crc/crc.py:4-88.
+
+Used by the codeblock-segmentation and DL-SCH host chain and by the BLER harness; the GPU
+CRC is a "next" item.  Same call surface: nr_crc_encode(blk, poly, mask=0)
+-> int8 blk ++ crc, nr_crc_decode(blkandcrc, poly, mask=0) -> (blk, err).
+"""
+import numpy as np
+
+_POLY = {  # generator coefficients x^(L-1) .. x^0 (crc.py:94-106)
+    "6": [1, 0, 0, 0, 0, 1],
+    "11": [1, 1, 0, 0, 0, 1, 0, 0, 0, 0, 1],
+    "16": [0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1],
+    "24A": [1, 0, 0, 0, 0, 1, 1, 0, 0, 1, 0, 0, 1, 1, 0, 0, 1, 1, 1, 1, 1, 0, 1, 1],
+    "24B": [1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 1, 1],
+    "24C": [1, 0, 1, 1, 0, 0, 1, 0, 1, 0, 1, 1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 1, 1, 1],
+}
+_TAB = {}
+
+
+def _table(poly):
+    """Byte-wise (MSB-first) CRC table for the generator."""
+    if poly not in _TAB:
+        p = _POLY[poly]
+        L = len(p)
+        g = int("".join(map(str, p)), 2)
+        top = 1 << (L - 1)
+        mask = (1 << L) - 1
+        tab = []
+        for byte in range(256):
+            reg = 0
+            for k in range(7, -1, -1):
+                fb = ((reg & top) != 0) ^ ((byte >> k) & 1)
+                reg = (reg << 1) & mask
+                if fb:
+                    reg ^= g
+            tab.append(reg)
+        _TAB[poly] = (L, tab)
+    return _TAB[poly]
+
+
+def _remainder(bits, poly):
+    """M(x) * x^L mod G(x) of the MSB-first bit sequence (crc.py:28-33 long division)."""
+    L, tab = _table(poly)
+    n = bits.size
+    head = n % 8
+    reg = 0
+    mask = (1 << L) - 1
+    g = int("".join(map(str, _POLY[poly])), 2)
+    top = 1 << (L - 1)
+    for b in bits[:head].tolist():   # leading bits one at a time
+        fb = ((reg & top) != 0) ^ (b & 1)
+        reg = (reg << 1) & mask
+        if fb:
+            reg ^= g
+    if n > head:
+        by = np.packbits(bits[head:].astype(np.uint8)).tolist()
+        if L >= 8:
+            sh = L - 8
+            for x in by:
+                reg = ((reg << 8) & mask) ^ tab[((reg >> sh) ^ x) & 0xFF]
+        else:
+            for x in by:
+                for k in range(7, -1, -1):
+                    fb = ((reg & top) != 0) ^ ((x >> k) & 1)
+                    reg = (reg << 1) & mask
+                    if fb:
+                        reg ^= g
+    return reg, L
+
+
+def _mask_bits(mask, L):
+    return mask & ((1 << L) - 1)   # LSB L bits of the (24-bit MSB-first) mask, crc.py:35-38
+
+
+def nr_crc_encode(blk, poly, mask=0):
+    blk = np.asarray(blk)
+    assert (not np.any(np.nonzero(blk < 0))) and (not np.any(np.nonzero(blk > 1)))
+    poly = poly.upper()
+    assert poly in _POLY
+    rem, L = _remainder(blk.astype(np.int64), poly)
+    if mask:
+        rem ^= _mask_bits(mask, L)
+    out = np.zeros(blk.size + L, "i1")
+    out[:blk.size] = blk
+    out[blk.size:] = [(rem >> (L - 1 - i)) & 1 for i in range(L)]
+    return out
+
+
+def nr_crc_decode(blkandcrc, poly, mask=0):
+    x = np.asarray(blkandcrc)
+    assert (not np.any(np.nonzero(x < 0))) and (not np.any(np.nonzero(x > 1)))
+    x = x.astype("i1")
+    poly = poly.upper()
+    assert poly in _POLY
+    L = len(_POLY[poly])
+    A = x.size - L
+    blk = x[0:A]
+    rem, _ = _remainder(x[:A].astype(np.int64), poly)
+    if mask:
+        rem ^= _mask_bits(mask, L)
+    tx = 0
+    for b in x[A:].tolist():
+        tx = (tx << 1) | int(b)
+    return blk, int(rem != tx)

@@ -1,0 +1,298 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE (py5gphy) in this
+container.  The reference never travels: only the input/output vectors below are committed.
+
+    cd /root/reference && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/gen_golden.py
+
+(the reference opens its tables through the relative path "py5gphy/ldpc/tables/",
+py5gphy/ldpc/ldpc_info.py:110, so the cwd must be the reference root.)
+
+Fixtures (all bit vectors stored np.packbits-packed, LLRs as float32 — the reference is run on
+the float64 widening of those float32 values so the fixtures are exact for both precisions):
+  encode_golden.npz    encode_ldpc (nr_ldpc_encode.py:8) on 51 Zc x 2 BG x 2 seeds, with fillers
+  decode_golden.npz    nr_decode_ldpc (nr_ldpc_decode.py:11), min-sum family, flooding, incl.
+                       rate-recovered LLRs (zeros, repetition averages, filler 10*max), integer
+                       LLRs (ties), all-zero LLRs, and 3 BG1 Zc=384 codeblocks
+  ratematch_golden.npz ratematch_ldpc / raterecover_ldpc / get_k0 / get_Er cases
+  crc_golden.json      CRC KATs (the inline vectors of py5gphy/crc/crc.py:167-210) + generated
+  dlsch_golden.npz     DLSCHEncode (nr_dlsch.py:12) transport blocks -> g_seq
+"""
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+sys.path.insert(0, REF)
+
+ZLIST = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 26, 28, 30, 32, 36,
+         40, 44, 48, 52, 56, 60, 64, 72, 80, 88, 96, 104, 112, 120, 128, 144, 160, 176, 192, 208,
+         224, 240, 256, 288, 320, 352, 384]
+
+
+def _ref():
+    from py5gphy.ldpc import nr_ldpc_encode, nr_ldpc_decode
+    return nr_ldpc_encode, nr_ldpc_decode
+
+
+def bpsk_llr(dn, snr_db, rng):
+    en = 1 - 2 * np.asarray(dn, np.float64)
+    fn = en + rng.normal(0, 10 ** (-snr_db / 20), en.shape)
+    return 2 * fn / 10 ** (-snr_db / 10)
+
+
+# ------------------------------------------------------------------------------------- encode
+def gen_encode():
+    enc, _ = _ref()
+    rng = np.random.default_rng(20251003)
+    meta, ckp, dnp = [], [], []
+    for bg in (1, 2):
+        kb = 22 if bg == 1 else 10
+        for Zc in ZLIST:
+            K = kb * Zc
+            for seed in range(2):
+                ck = rng.integers(0, 2, K).astype(np.int8)
+                F = 0 if seed == 0 else int(rng.integers(1, K - 2 * Zc))
+                if F:
+                    ck[K - F:] = -1
+                ck_in = ck.copy()
+                dn = enc.encode_ldpc(ck_in, bg)
+                # reference semantics pinned here: systematic part copied (fillers stay -1) ...
+                assert np.array_equal(dn[:K - 2 * Zc], ck[2 * Zc:])
+                # ... and fillers zeroed in the caller's array in place (nr_ldpc_encode.py:34-35)
+                exp_in = ck.copy()
+                exp_in[2 * Zc:][exp_in[2 * Zc:] == -1] = 0
+                assert np.array_equal(ck_in, exp_in)
+                par = dn[K - 2 * Zc:]
+                assert set(np.unique(par)) <= {0, 1}
+                meta.append((bg, Zc, F))
+                ckp.append(np.packbits(ck == 1))
+                dnp.append(np.packbits(par == 1))
+    np.savez_compressed(os.path.join(OUT, "encode_golden.npz"), meta=np.array(meta, np.int32),
+                        ck_bits=np.concatenate(ckp), ck_off=_offs(ckp),
+                        par_bits=np.concatenate(dnp), par_off=_offs(dnp))
+    print("encode cases", len(meta))
+
+
+def _offs(lst):
+    return np.concatenate([[0], np.cumsum([x.size for x in lst])]).astype(np.int64)
+
+
+# ------------------------------------------------------------------------------------- decode
+def _decode_case(args):
+    (bg, Zc, L, alpha, beta, llr32) = args
+    _, dec = _ref()
+    t = time.time()
+    _, ck, status = dec.nr_decode_ldpc(llr32.astype(np.float64), Zc, bg, L, "min-sum", alpha, beta)
+    return np.packbits(ck == 1), bool(status), time.time() - t
+
+
+def _mk_awgn(rng, bg, Zc, snr):
+    import oracle_shim as O
+    K = (22 if bg == 1 else 10) * Zc
+    ck = rng.integers(0, 2, K).astype(np.int8)
+    dn = O.encode(ck, bg)
+    return bpsk_llr(dn, snr, rng).astype(np.float32)
+
+
+def _mk_ratematched(rng, bg):
+    """LLRs as the DL-SCH receiver builds them: ratematch -> BPSK+AWGN -> raterecover
+    (nr_ldpc_ratematch.py:64 / nr_ldpc_raterecover.py:6) — exact zeros for punctured bits,
+    averaged repetitions, 10*max|LLR| on filler positions."""
+    from py5gphy.ldpc import ldpc_info, nr_ldpc_ratematch as RM, nr_ldpc_raterecover as RR
+    import oracle_shim as O
+    while True:
+        B = int(rng.integers(60, 3000))
+        try:
+            C, cbz, Lc, F, K, Zc = ldpc_info.get_cbs_info(B, bg)
+            break
+        except AssertionError:
+            pass
+    if Zc > 96:
+        return None
+    K_apo = K - F
+    ck = rng.integers(0, 2, K).astype(np.int8)
+    ck[K_apo:] = -1
+    dn = O.encode(ck, bg)
+    N = dn.size
+    Ncb = N if rng.random() < 0.6 else int(rng.integers(K, N + 1))
+    Qm = int(rng.choice([1, 2, 4, 6, 8]))
+    rv = int(rng.integers(0, 4))
+    E = Qm * int(rng.integers(max(1, (K - F) // Qm), int(1.7 * N) // Qm))
+    k0 = RM.get_k0(Ncb, bg, rv, Zc)
+    fe = RM.ratematch_ldpc(dn, Ncb, E, k0, Qm)
+    snr = float(rng.uniform(-1, 3))
+    y = bpsk_llr(fe, snr, rng)
+    llr = RR.raterecover_ldpc(y, Ncb, N, k0, Qm, Zc, K_apo, K)
+    return Zc, llr.astype(np.float32)
+
+
+def gen_decode(pool):
+    rng = np.random.default_rng(77)
+    zs = [2, 3, 4, 5, 6, 7, 9, 11, 13, 15, 16, 24, 28, 36, 44, 52, 60, 72]
+    ab = [(1.0, 0.0), (0.75, 0.0), (1.0, 0.5), (0.8, 0.3)]
+    cases = []   # (kind, bg, Zc, L, alpha, beta, llr32)
+    i = 0
+    for bg in (1, 2):
+        for zi, Zc in enumerate(zs):
+            for k in range(4):
+                snr = [-1.0, 0.0, 1.0, 2.0][(zi + k) % 4]
+                a, b = ab[(zi + 2 * k) % 4]
+                L = [8, 32][(zi + k) % 2]
+                cases.append(("awgn", bg, Zc, L, a, b, _mk_awgn(rng, bg, Zc, snr)))
+                i += 1
+    n = 0
+    while n < 32:
+        bg = 1 + n % 2
+        r = _mk_ratematched(rng, bg)
+        if r is None:
+            continue
+        Zc, llr = r
+        a, b = ab[n % 4]
+        cases.append(("ratematched", bg, Zc, [8, 16][n % 2], a, b, llr))
+        n += 1
+    # integer-valued LLRs: many exact ties in the two-min selection (tie rules :195-199)
+    for n in range(12):
+        bg = 1 + n % 2
+        Zc = [4, 6, 10, 12, 20, 26][n % 6]
+        K = (22 if bg == 1 else 10) * Zc
+        import oracle_shim as O
+        dn = O.encode(rng.integers(0, 2, K).astype(np.int8), bg)
+        llr = (1 - 2 * dn.astype(np.float32)) * rng.integers(1, 4, dn.size)
+        flip = rng.random(dn.size) < 0.12
+        llr[flip] = -llr[flip]
+        zero = rng.random(dn.size) < 0.05
+        llr[zero] = 0
+        cases.append(("ties", bg, Zc, 8, *ab[n % 4], llr.astype(np.float32)))
+    # all-zero LLRs: decision 0, syndrome 0 -> immediate success (nr_ldpc_decode.py:107-114)
+    for bg, Zc in ((1, 8), (2, 15)):
+        N = (66 if bg == 1 else 50) * Zc
+        cases.append(("zeros", bg, Zc, 8, 1.0, 0.0, np.zeros(N, np.float32)))
+    print("decode cases (small)", len(cases))
+    t = time.time()
+    res = pool.map(_decode_case, [c[1:] for c in cases], chunksize=1)
+    print("small decode done", time.time() - t)
+    # 3 full-size BG1 Zc=384 codeblocks (the BASELINE config-3 shape), run serially (7.7 GB each)
+    big = [(0.5, 0.75, 0.0), (-2.0, 0.75, 0.0), (1.5, 1.0, 0.0)]
+    for snr, a, b in big:
+        llr = _mk_awgn(rng, 1, 384, snr)
+        cases.append(("z384", 1, 384, 8, a, b, llr))
+        r = _decode_case((1, 384, 8, a, b, llr))
+        print("z384 snr", snr, "status", r[1], "t", round(r[2], 1))
+        res.append(r)
+    kinds = sorted(set(c[0] for c in cases))
+    np.savez_compressed(
+        os.path.join(OUT, "decode_golden.npz"),
+        kind=np.array([kinds.index(c[0]) for c in cases], np.int8), kinds=np.array(kinds),
+        bg=np.array([c[1] for c in cases], np.int32), Zc=np.array([c[2] for c in cases], np.int32),
+        L=np.array([c[3] for c in cases], np.int32), alpha=np.array([c[4] for c in cases]),
+        beta=np.array([c[5] for c in cases]),
+        llr=np.concatenate([c[6] for c in cases]), llr_off=_offs([c[6] for c in cases]),
+        ck_bits=np.concatenate([r[0] for r in res]), ck_off=_offs([r[0] for r in res]),
+        status=np.array([r[1] for r in res]))
+    print("decode cases", len(cases), "status True", sum(r[1] for r in res))
+
+
+# --------------------------------------------------------------------------- rate matching
+def gen_ratematch():
+    from py5gphy.ldpc import ldpc_info, nr_ldpc_ratematch as RM, nr_ldpc_raterecover as RR
+    import oracle_shim as O
+    rng = np.random.default_rng(5)
+    rows = []
+    dns, fes, llrs, rrs = [], [], [], []
+    n = 0
+    while n < 16:
+        bg = 1 + n % 2
+        B = int(rng.integers(100, 3000))
+        try:
+            C, cbz, Lc, F, K, Zc = ldpc_info.get_cbs_info(B, bg)
+        except AssertionError:
+            continue
+        K_apo = K - F
+        ck = rng.integers(0, 2, K).astype(np.int8)
+        ck[K_apo:] = -1
+        dn = O.encode(ck, bg)
+        N = dn.size
+        Ncb = N if n % 3 else int(rng.integers(K, N + 1))
+        Qm = [1, 2, 4, 6, 8][n % 5]
+        rv = n % 4
+        E = Qm * int(rng.integers(max(1, K // (2 * Qm)), int(1.8 * N) // Qm))
+        k0 = RM.get_k0(Ncb, bg, rv, Zc)
+        fe = RM.ratematch_ldpc(dn, Ncb, E, k0, Qm)
+        y = rng.normal(size=E).astype(np.float32).astype(np.float64)   # stored as float32
+        rr = RR.raterecover_ldpc(y, Ncb, N, k0, Qm, Zc, K_apo, K)
+        rows.append((bg, Zc, K, K_apo, N, Ncb, E, k0, Qm, rv))
+        dns.append(dn)
+        fes.append(fe)
+        llrs.append(y)
+        rrs.append(rr)
+        n += 1
+    er = []
+    for G, C, Qm, NL in [(100000, 5, 2, 1), (36036 * 8 * 4, 129, 8, 4), (12345 * 6, 7, 6, 1),
+                         (24000, 3, 4, 2)]:
+        er.append((G, C, Qm, NL, RM.get_Er_ldpc(G, C, Qm, NL)))
+    np.savez_compressed(os.path.join(OUT, "ratematch_golden.npz"),
+                        meta=np.array(rows, np.int64),
+                        dn=np.concatenate(dns), dn_off=_offs(dns),
+                        fe=np.concatenate(fes), fe_off=_offs(fes),
+                        llr=np.concatenate(llrs).astype(np.float32), llr_off=_offs(llrs),
+                        rr=np.concatenate(rrs), rr_off=_offs(rrs))
+    with open(os.path.join(OUT, "er_golden.json"), "w") as f:
+        json.dump([{"G": a, "C": b, "Qm": c, "NL": d, "Er": e} for a, b, c, d, e in er], f)
+    print("ratematch cases", len(rows))
+
+
+# -------------------------------------------------------------------------------------- CRC
+def gen_crc():
+    from py5gphy.crc import crc
+    rng = np.random.default_rng(9)
+    out = []
+    for poly in ["6", "11", "16", "24A", "24B", "24C"]:
+        for mask in (0, 1, 12345, 45678):
+            for n in (1, 8, 37, 200):
+                blk = rng.integers(0, 2, n)
+                out.append({"poly": poly, "mask": mask, "blk": blk.tolist(),
+                            "out": crc.nr_crc_encode(blk, poly, mask).tolist()})
+    with open(os.path.join(OUT, "crc_golden.json"), "w") as f:
+        json.dump(out, f)
+    print("crc cases", len(out))
+
+
+# ------------------------------------------------------------------------------------ DL-SCH
+def gen_dlsch():
+    from py5gphy.nr_pdsch import nr_dlsch
+    rng = np.random.default_rng(11)
+    rows, tbs, gs = [], [], []
+    # (TBS, Qm, R*1024, NL, rv, TBS_LBRM, G): a BG2 single-CB TB and BG1 multi-CB TBs
+    for TBS, Qm, R, NL, rv, LBRM, G in [(1800, 2, 308, 1, 0, 40000, 6000),
+                                        (24000, 6, 658, 2, 1, 100000, 40008),
+                                        (12000, 4, 517, 1, 2, 30000, 25000)]:
+        trblk = rng.integers(0, 2, TBS)
+        g = nr_dlsch.DLSCHEncode(trblk, TBS, Qm, R, NL, rv, LBRM, G)
+        rows.append((TBS, Qm, R, NL, rv, LBRM, G))
+        tbs.append(np.packbits(trblk.astype(np.uint8)))
+        gs.append(np.packbits(g == 1))
+    np.savez_compressed(os.path.join(OUT, "dlsch_golden.npz"), meta=np.array(rows, np.int64),
+                        tb=np.concatenate(tbs), tb_off=_offs(tbs),
+                        g=np.concatenate(gs), g_off=_offs(gs))
+    print("dlsch cases", len(rows))
+
+
+if __name__ == "__main__":
+    os.chdir(REF)
+    sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
+    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "decode"]
+    if "encode" in which:
+        gen_encode()
+    if "crc" in which:
+        gen_crc()
+    if "ratematch" in which:
+        gen_ratematch()
+    if "dlsch" in which:
+        gen_dlsch()
+    if "decode" in which:
+        with mp.get_context("fork").Pool(6) as pool:
+            gen_decode(pool)

@@ -1,0 +1,169 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports every declared
+symbol, argument validation maps to the reference's AssertionError, and the host-side
+reference mirrors (ldpc_info, crc, segmentation, rate matching) match the golden vectors.
+No kernel is launched here (no GPU in the build container)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, ROOT, load_json
+from oracle import ldpc_oracle as O
+from python_5gtoolbox_amd import _lib, crc, ldpc_info, nr_ldpc_cbsegment
+from python_5gtoolbox_amd import nr_ldpc_ratematch as RM
+from python_5gtoolbox_amd import nr_ldpc_raterecover as RR
+
+HEADER = os.path.join(ROOT, "include", "ldpc5g.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ldpc5g_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    names = declared_functions()
+    assert set(names) == set(_lib.SIGNATURES), names
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.ldpc5g_version().startswith(b"ldpc5g")
+
+
+def test_header_constants_match_binding():
+    src = open(HEADER).read()
+    consts = dict(re.findall(r"#define (LDPC5G_\w+) \(?(-?\d+)\)?", src))
+    assert int(consts["LDPC5G_F64"]) == _lib.F64 and int(consts["LDPC5G_F32"]) == _lib.F32
+    assert int(consts["LDPC5G_FLOODING"]) == _lib.FLOODING
+    assert int(consts["LDPC5G_LAYERED"]) == _lib.LAYERED
+    assert int(consts["LDPC5G_LLR_FULL"]) == _lib.LLR_FULL
+    assert int(consts["LDPC5G_EBGN"]) == _lib.EBGN and int(consts["LDPC5G_EZC"]) == _lib.EZC
+    assert ctypes.sizeof(_lib.CbDesc) == 24
+
+
+def test_find_ils_abi_matches_reference_table():
+    lib = _lib.lib()
+    for z in range(1, 400):
+        assert lib.ldpc5g_find_ils(z) == ldpc_info.find_iLS(z) == O.find_iLS(z)
+
+
+@pytest.mark.parametrize("call,code", [
+    (lambda l: l.ldpc5g_encode(None, None, 1, 3, 384, 8448, 25344, None), _lib.EBGN),
+    (lambda l: l.ldpc5g_encode(None, None, 1, 1, 383, 8448, 25344, None), _lib.EZC),
+    (lambda l: l.ldpc5g_encode(None, None, 1, 1, 384, 8000, 25344, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_ms(None, 0, None, None, None, 1, 1, 384, 8, 1.0, 0.0, 0, 0,
+                                  25344, 26112, None), _lib.ESIZE),   # null buffers
+    (lambda l: l.ldpc5g_decode_ms(None, 0, None, None, None, 1, 1, 384, 8, 1.0, 0.0, 1, 0,
+                                  25344, 26112, None), _lib.ESIZE),   # layered needs F32
+    (lambda l: l.ldpc5g_decode_ms(None, 1, None, None, None, 1, 2, 10, 8, 1.0, 0.0, 0, 0,
+                                  499, 520, None), _lib.ESIZE),       # ldl < N
+    (lambda l: l.ldpc5g_decode_ms(None, 1, None, None, None, 4, 2, 1, 8, 1.0, 0.0, 0, 0,
+                                  500, 520, None), _lib.EZC),
+    (lambda l: l.ldpc5g_encode(None, None, 0, 1, 384, 8448, 25344, None), 0),   # empty batch
+])
+def test_abi_validation_without_gpu(call, code):
+    """Argument checks run before any HIP call and return the documented codes."""
+    lib = _lib.lib()
+    assert call(lib) == code
+    if code:
+        assert lib.ldpc5g_last_error()
+        with pytest.raises(AssertionError):
+            _lib.check(code)
+
+
+def test_mixed_abi_validation_without_gpu():
+    lib = _lib.lib()
+    d = (_lib.CbDesc * 2)()
+    d[0].bgn, d[0].Zc = 1, 384
+    d[1].bgn, d[1].Zc = 3, 384
+    dummy = ctypes.c_void_p(16)
+    rc = lib.ldpc5g_decode_ms_mixed(d, 2, dummy, 1, dummy, dummy, dummy, 8, 1.0, 0.0, 0, 0, None)
+    assert rc == _lib.EBGN
+    d[1].bgn, d[1].Zc = 2, 7
+    d[0].Zc = 385
+    assert lib.ldpc5g_decode_ms_mixed(d, 2, dummy, 1, dummy, dummy, dummy, 8, 1.0, 0.0, 0, 0,
+                                      None) == _lib.EZC
+
+
+def test_ldpc_info_mirror():
+    for B in [100, 292, 3824, 8424, 8448, 8449, 20000, 1081536]:
+        for bg in (1, 2):
+            try:
+                ref = O.get_cbs_info(B, bg)
+            except AssertionError:
+                with pytest.raises(AssertionError):
+                    ldpc_info.get_cbs_info(B, bg)
+                continue
+            assert ldpc_info.get_cbs_info(B, bg) == ref
+    for bg, Zc in [(1, 2), (2, 3), (1, 13), (2, 15)]:
+        H = ldpc_info.getH(Zc, bg, ldpc_info.find_iLS(Zc))
+        assert np.array_equal(H, O.getH(Zc, bg))
+        assert ldpc_info.match_H(H) == (bg, Zc)
+        H2 = H.copy()
+        H2[0, 0] ^= 1
+        assert ldpc_info.match_H(H2) is None
+
+
+def test_crc_mirror_golden():
+    for c in load_json("crc_golden.json"):
+        out = crc.nr_crc_encode(np.array(c["blk"]), c["poly"], c["mask"])
+        assert out.tolist() == c["out"]
+        blk, err = crc.nr_crc_decode(out, c["poly"], c["mask"])
+        assert err == 0 and blk.tolist() == c["blk"]
+        bad = out.copy()
+        bad[len(bad) // 2] ^= 1
+        assert crc.nr_crc_decode(bad, c["poly"], c["mask"])[1] == 1
+
+
+def test_crc_inline_kats():
+    """Known answers held inline by the reference (py5gphy/crc/crc.py:167-210)."""
+    kats = [("6", [1, 1, 1, 1], 0, [1, 1, 1, 1, 0, 0, 1, 0, 1, 0]),
+            ("6", [1, 0, 1, 1, 0, 1, 1, 0, 1], 45678, [1, 0, 1, 1, 0, 1, 1, 0, 1, 0, 1, 1, 1, 0, 0]),
+            ("11", [1, 0, 1, 1], 12345, [1, 0, 1, 1, 0, 1, 1, 1, 1, 0, 1, 0, 1, 1, 0]),
+            ("24A", [0, 0, 1, 1, 0, 0, 0, 1], 45678,
+             [0, 0, 1, 1, 0, 0, 0, 1, 0, 1, 0, 0, 1, 1, 1, 1, 0, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1, 0, 1, 0, 1]),
+            ("24B", [0, 0, 1, 1, 0, 0, 0, 1], 0,
+             [0, 0, 1, 1, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1]),
+            ("24C", [0, 0, 1, 1, 0, 0, 0, 1], 45678,
+             [0, 0, 1, 1, 0, 0, 0, 1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 1, 1, 0, 0, 1, 0, 1, 1, 1, 0, 0, 0, 1, 0, 1])]
+    for poly, blk, mask, exp in kats:
+        assert crc.nr_crc_encode(np.array(blk), poly, mask).tolist() == exp
+        assert O.crc_encode(np.array(blk), poly, mask).tolist() == exp
+
+
+def test_ratematch_mirror_golden():
+    d = np.load(os.path.join(GOLD, "ratematch_golden.npz"))
+    for i, (bg, Zc, K, K_apo, N, Ncb, E, k0, Qm, rv) in enumerate(d["meta"].tolist()):
+        dn = d["dn"][d["dn_off"][i]:d["dn_off"][i + 1]]
+        assert RM.get_k0(Ncb, bg, rv, Zc) == k0
+        assert np.array_equal(RM.ratematch_ldpc(dn, Ncb, E, k0, Qm),
+                              d["fe"][d["fe_off"][i]:d["fe_off"][i + 1]])
+        llr = d["llr"][d["llr_off"][i]:d["llr_off"][i + 1]].astype(np.float64)
+        assert np.array_equal(RR.raterecover_ldpc(llr, Ncb, N, k0, Qm, Zc, K_apo, K),
+                              d["rr"][d["rr_off"][i]:d["rr_off"][i + 1]])
+    for c in load_json("er_golden.json"):
+        assert RM.get_Er_ldpc(c["G"], c["C"], c["Qm"], c["NL"]) == c["Er"]
+
+
+def test_cbsegment_mirror():
+    rng = np.random.default_rng(1)
+    for B, bg in [(3000, 2), (30000, 1), (8448, 1), (500, 2)]:
+        x = rng.integers(0, 2, B)
+        a, za = nr_ldpc_cbsegment.ldpc_cbsegment(x, bg)
+        b, zb = O.cbsegment(x, bg)
+        assert za == zb and np.array_equal(a, b)
+
+
+def test_product_fails_loudly_without_gpu():
+    """No CPU fallback: the GPU entry points raise when no GPU is visible."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from python_5gtoolbox_amd import nr_ldpc_decode, nr_ldpc_encode
+    with pytest.raises(_lib.LdpcLibError):
+        nr_ldpc_encode.encode_ldpc(np.zeros(80, np.int8), 2)
+    with pytest.raises(_lib.LdpcLibError):
+        nr_ldpc_decode.nr_decode_ldpc(np.zeros(400), 8, 2, 8)
