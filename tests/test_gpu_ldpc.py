@@ -143,7 +143,7 @@ def test_decode_packed_workgroups(torch, dec, bg, Zc, schedule):
     B = 200
     ck = rng.integers(0, 2, (B, K)).astype(np.int8)
     dn = O.encode(ck, bg)
-    snr = rng.uniform(-1.5, 3.0, (B, 1))
+    snr = rng.uniform(-3.0, 2.5, (B, 1))
     llr = (2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
            10 ** (-snr / 10)).astype(np.float32)
     got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 12, "min-sum", 0.8, 0.1, schedule)
@@ -151,7 +151,7 @@ def test_decode_packed_workgroups(torch, dec, bg, Zc, schedule):
            else O.decode_flooding(llr, Zc, bg, 12, 0.8, 0.1, np.float32))
     for g, r in zip(got, ref):
         assert np.array_equal(g, r)
-    assert 0 < got[1].sum() < B    # a mix of converged and failed codeblocks
+    assert got[1].sum() > 0 and len(np.unique(got[2])) > 2   # early exits at different iterations
 
 
 @pytest.mark.parametrize("schedule", ["flooding", "layered"])
