@@ -296,11 +296,11 @@ def decode_layered(llr, Zc, bgn, L, alpha=1.0, beta=0.0):
       APP = [0]*2Zc ++ llr on the Kb+4 core columns; degree-1 extension columns keep no APP:
       their variable-to-check message is the channel LLR itself and APP = llr + r.
       per iteration, per base row i (layer):
-         app_old = APP[c] (ext: llr + r_old);  q = app_old - r_old (ext: q = llr)
-         r_new = CN(q) (same CN as the flooding path);  APP[c] = q + r_new (ext: llr + r_new)
-      convergence after an iteration in which every row's parity (on app_old) held and no hard
-      decision (APP < 0) flipped -> ck = APP < 0, status True, iters = it+1.
-      after L iterations without convergence: ck = APP <= 0, status = syndrome == 0, iters = L."""
+         q = APP[c] - r_old (ext: q = llr);  r_new = CN(q) (same CN as the flooding path)
+         APP[c] = q + r_new (ext: llr + r_new)
+      stopping rule, after each iteration: if no hard decision (APP < 0) changed over the
+      iteration and the hard decisions satisfy every check -> ck = APP < 0, status True,
+      iters = it+1.  After L iterations: ck = APP <= 0, status = syndrome == 0, iters = L."""
     T = np.float32
     llr = np.atleast_2d(np.asarray(llr)).astype(T)
     g = graph(bgn, Zc)
@@ -322,33 +322,28 @@ def decode_layered(llr, Zc, bgn, L, alpha=1.0, beta=0.0):
             a[:, cols] = Lfull[:, cols] + R[i][:, -1]
         return a
 
+    hd_prev = cur_app() < 0
     for it in range(L):
         act = ~done
-        fail = np.zeros(B, bool)
-        flip = np.zeros(B, bool)
         for i in range(g.Mb):
             cols = g.rows_cols(i)                       # (d, Zc)
             core = g.bj[g.rs[i]:g.rs[i + 1]] < g.Kcore  # (d,)
-            app_old = APP[:, cols].copy()
-            app_old[:, ~core] = Lfull[:, cols[~core]] + R[i][:, ~core]
-            q = app_old - R[i]
+            q = APP[:, cols] - R[i]
             q[:, ~core] = Lfull[:, cols[~core]]
-            fail |= np.bitwise_xor.reduce(app_old < 0, axis=1).any(axis=1)
             r = _cn_update(q, alpha, beta, T)
             app_new = q + r
-            app_new[:, ~core] = Lfull[:, cols[~core]] + r[:, ~core]
-            flip |= ((app_new < 0) != (app_old < 0)).any(axis=(1, 2))
-            upd = act
             cc = cols[core]
-            APP[np.ix_(upd, cc.reshape(-1))] = app_new[upd][:, core].reshape(upd.sum(), -1)
-            R[i][upd] = r[upd]
-        conv = act & ~fail & ~flip
-        if conv.any():
-            a = cur_app()
-            ck[conv] = (a < 0)[conv]
+            APP[np.ix_(act, cc.reshape(-1))] = app_new[act][:, core].reshape(act.sum(), -1)
+            R[i][act] = r[act]
+        hd = cur_app() < 0
+        cand = act & (hd == hd_prev).all(axis=1)
+        if cand.any():
+            conv = cand & ~_row_hd_fail(hd, g)
+            ck[conv] = hd[conv]
             status[conv] = True
             iters[conv] = it + 1
             done |= conv
+        hd_prev = hd
         if done.all():
             break
     rem = ~done

@@ -65,10 +65,14 @@ constexpr int edge_of(int i, int j) {
     return -1;
 }
 
+// V(i,j) mod Zc of edge e for lifting size index zi (tables packed 2 edges per 32-bit word so a
+// wave-uniform read is a scalar load)
 template <int BG>
-__device__ __forceinline__ const uint16_t* shift_table(int zi) {
-    if constexpr (BG == 1) return kBG1ShiftMod[zi];
-    else return kBG2ShiftMod[zi];
+__device__ __forceinline__ int shift_of(int zi, int e) {
+    uint32_t w;
+    if constexpr (BG == 1) w = kBG1ShiftMod[zi][e >> 1];
+    else w = kBG2ShiftMod[zi][e >> 1];
+    return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
 }
 template <int BG>
 __device__ __forceinline__ int row_start_d(int i) {
@@ -182,8 +186,6 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
     uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
     uint32_t* PB = pv + 5 * W;
     int8_t* raw = (int8_t*)(sm + Ly.words);
-    const uint16_t* sh = shift_table<BG>(zi);
-
     // ---- 1. load info bytes, keep them raw in LDS, pack parity bits (fillers -> 0)
     const int8_t* src = ck + (int64_t)b * ldk;
     const bool al16 = (((uintptr_t)src) & 15) == 0;
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
         uint32_t acc = 0;
         for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
             int j = col_d<BG>(e);
-            if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + sh[e]);
+            if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
         }
         lam[i * W + w] = acc;
     }
@@ -259,19 +261,19 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
     // (window reads one word past a vector; those bits are masked, the word exists in LDS)
     __syncthreads();
     {
-        const int s1 = sh[eS];
+        const int s1 = shift_of<BG>(zi, eS);
         // p1 = roll(L2, s1): p1[z] = L2[(z - s1) mod Zc]
         for (int w = t; w < W; w += NT) p1[w] = fetch_rot32(L2, 0, Zc, mod_zc(mod_zc(32 * w, Zc) + Zc - s1, Zc));
     }
     __syncthreads();
     for (int w = t; w < W; w += NT) {
-        p2[w] = lam[w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + sh[eA], Zc));
-        p4[w] = lam[3 * W + w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + sh[eC], Zc));
+        p2[w] = lam[w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eA), Zc));
+        p4[w] = lam[3 * W + w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eC), Zc));
     }
     __syncthreads();
     for (int w = t; w < W; w += NT) {
-        if constexpr (BG == 1) p3[w] = lam[2 * W + w] ^ fetch_rot32(p4, 0, Zc, mod_zc(32 * w + sh[eD], Zc));
-        else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + sh[eD], Zc));
+        if constexpr (BG == 1) p3[w] = lam[2 * W + w] ^ fetch_rot32(p4, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+        else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
     }
     __syncthreads();
 
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
         uint32_t acc = 0;
         for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
             int j = col_d<BG>(e);
-            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + sh[e]);
+            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
         }
         or_bits(PB, i * Zc + 32 * w, acc, min(32, Zc - 32 * w));
     }
@@ -342,26 +344,64 @@ template <typename T>
 struct FT;
 template <>
 struct FT<float> {
-    __device__ static __forceinline__ float flip(float m, uint32_t neg) {
-        return __uint_as_float(__float_as_uint(m) ^ (neg << 31));
+    __device__ static __forceinline__ uint32_t sbits(float x) { return __float_as_uint(x); }
+    // x with its sign bit XORed by bit 31 of `b`
+    __device__ static __forceinline__ float xsign(float x, uint32_t b) {
+        return __uint_as_float(__float_as_uint(x) ^ (b & 0x80000000u));
     }
     __device__ static __forceinline__ float inf() { return __uint_as_float(0x7f800000u); }
+    __device__ static __forceinline__ float med3(float a, float b, float c) {
+        return __builtin_amdgcn_fmed3f(a, b, c);
+    }
 };
 template <>
 struct FT<double> {
-    __device__ static __forceinline__ double flip(double m, uint32_t neg) {
-        return __longlong_as_double(__double_as_longlong(m) ^ ((long long)neg << 63));
+    __device__ static __forceinline__ uint32_t sbits(double x) { return (uint32_t)__double2hiint(x); }
+    __device__ static __forceinline__ double xsign(double x, uint32_t b) {
+        return __longlong_as_double(__double_as_longlong(x) ^ ((long long)(b & 0x80000000u) << 32));
     }
     __device__ static __forceinline__ double inf() { return __longlong_as_double(0x7ff0000000000000ll); }
+    __device__ static __forceinline__ double med3(double a, double b, double c) {
+        return fmax(fmin(a, b), fmin(fmax(a, b), c));
+    }
 };
 
-// Compressed check-node state of one row: r_k = (k == idx ? mB : mA) with sign bit k of pk.
-// pk: bits 0..deg-1 = sign of r_k, bits 24..28 = idx (argmin of |q|).
+// Compressed check-node state of one row: r_k = (k == idx ? mB : mA), sign = bit k of pk.
+// pk: bits 0..deg-1 = sign of r_k, bits 24..28 = idx (an edge holding min |q|).
 template <typename T>
-__device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, int k) {
-    T m = (((pk >> 24) & 31u) == (uint32_t)k) ? mB : mA;
-    return FT<T>::flip(m, (pk >> k) & 1u);
+__device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, uint32_t idx, int k) {
+    return FT<T>::xsign((idx == (uint32_t)k) ? mB : mA, pk << (31 - k));
 }
+
+// Consecutive base rows with disjoint core columns form one barrier group: processing them
+// together is identical to processing them one after another (layered) and keeps the
+// row-ascending accumulation order of every column (flooding).  BG1: 46 rows -> 32 groups,
+// BG2: 42 -> 28.
+template <int BG>
+struct RowGroups {
+    int n = 0;
+    int start[64] = {};
+    constexpr RowGroups() {
+        using P = BGT<BG>;
+        int g0 = 0;
+        start[0] = 0;
+        n = 1;
+        for (int i = 1; i < P::MB; ++i) {
+            bool dis = true;
+            for (int a = g0; a < i && dis; ++a)
+                for (int e = P::RS[a]; e < P::RS[a + 1]; ++e)
+                    for (int f = P::RS[i]; f < P::RS[i + 1]; ++f)
+                        if (P::COL[e] == P::COL[f] && P::COL[e] < P::KC) dis = false;
+            if (!dis) {
+                start[n++] = i;
+                g0 = i;
+            }
+        }
+        start[n] = P::MB;
+    }
+};
+template <int BG>
+constexpr RowGroups<BG> kGroups{};
 
 struct DecWork {     // one workgroup of the mixed-Zc path
     int32_t zi, Zc, G, first;
@@ -371,7 +411,14 @@ struct CbRef {       // one codeblock of the mixed-Zc path
     int32_t out, pad;
 };
 
-constexpr int kDecThreads = 384;
+constexpr int kDecThreads = 384;   // = max Zc: one thread per check row z of a base row
+constexpr int kCS = kDecThreads;   // LDS column stride (entries): G*Zc <= 384 always
+
+template <typename T, bool LAYERED>
+constexpr size_t dec_lds_bytes_t(int MB, int KC) {
+    return (size_t)KC * kCS * sizeof(T) * (LAYERED ? 1 : 2) +
+           (sizeof(T) == 4 ? (size_t)(MB - 4) * kCS * sizeof(T) : 0) + 2 * kCS * sizeof(int);
+}
 
 template <int BG, typename T, bool LAYERED>
 __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
@@ -382,7 +429,11 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     // pc = number of leading punctured block columns absent from the LLR rows (2, or 0 when the
     // caller passes full-length rows as decode_ldpc(LLRin, H, ...) does, nr_ldpc_decode.py:51)
     using P = BGT<BG>;
-    constexpr int MB = P::MB, KB = P::KB, KC = P::KC;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
+    constexpr bool XL_LDS = TS == 4;
+    constexpr int ACC_B = KC * kCS * TS;                        // byte offsets in LDS
+    constexpr int XL_B = KC * kCS * TS * (LAYERED ? 1 : 2);
+    constexpr int FLAG_B = XL_B + (XL_LDS ? (MB - 4) * kCS * TS : 0);
     extern __shared__ __align__(16) unsigned char smem[];
 
     int Zc = Zc_u, zi = zi_u, G = G_u;
@@ -394,8 +445,8 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     const int cbl = t / Zc;
     const int z = t - cbl * Zc;
     bool valid = cbl < G;
-    const T* lrow = nullptr;
-    int8_t* crow = nullptr;
+    const T* lrow = llr;
+    int8_t* crow = ck;
     int out = 0;
     if (valid) {
         if (work) {
@@ -412,17 +463,17 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         }
     }
     const int cl = valid ? cbl : 0;
-    // LDS: app[G][KC][Zc] | acc[G][KC][Zc] (flooding) | xl[G][MB-4][Zc] (fp32) | flag[G]
-    constexpr bool XL_LDS = sizeof(T) == 4;
-    T* app = (T*)smem + (size_t)cl * KC * Zc;
-    T* acc = (T*)smem + (size_t)G * KC * Zc + (size_t)cl * KC * Zc;   // flooding only
-    T* xl = (T*)smem + (size_t)G * KC * Zc * (LAYERED ? 1 : 2) + (size_t)cl * (MB - 4) * Zc;
-    int* flag = (int*)((T*)smem + (size_t)G * KC * Zc * (LAYERED ? 1 : 2) +
-                       (XL_LDS ? (size_t)G * (MB - 4) * Zc : 0));
-    const uint16_t* sh = shift_table<BG>(zi);
-    // channel LLR of the degree-1 extension column owned by row (i, z): LDS for fp32, the
-    // caller's (L2-resident) row for fp64, whose LDS is filled by app + acc
-    auto llrx = [&](int i4) -> T { return XL_LDS ? xl[i4 * Zc + z] : lrow[(KB + 4 + i4 - pc) * Zc + z]; };
+    const int tzb = (cl * Zc + z) * TS;   // byte offset of this thread's own column entry
+    const int ZcT = Zc * TS;
+    int* flagA = (int*)(smem + FLAG_B);
+    int* flagB = flagA + kCS;
+    auto at = [&](int byte) -> T& { return *(T*)(smem + byte); };
+    auto own = [&](int j) -> T& { return at(j * kCS * TS + tzb); };
+    // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
+    auto llrx = [&](int i4) -> T {
+        if constexpr (XL_LDS) return at(XL_B + i4 * kCS * TS + tzb);
+        else return lrow[(KB + 4 + i4 - pc) * Zc + z];
+    };
 
     // per-thread state of rows (i, z), i = 0..MB-1
     T sA[MB], sB[MB];
@@ -430,137 +481,186 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
 #pragma unroll
     for (int i = 0; i < MB; ++i) sA[i] = T(0), sB[i] = T(0), sP[i] = 0u;
 
+    uint32_t hdc_prev = 0;   // layered: hard decisions of own core columns, last iteration end
+    uint64_t hdx_prev = 0;   // layered: ... of own extension columns
     if (valid) {
         for (int j = 0; j < KC; ++j) {
-            T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
-            app[j * Zc + z] = v;
-            if (!LAYERED) acc[j * Zc + z] = T(0);
+            const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
+            own(j) = v;
+            if (!LAYERED) at(ACC_B + j * kCS * TS + tzb) = T(0);
+            hdc_prev |= (uint32_t)(v < T(0)) << j;
         }
-        if (XL_LDS)
-            for (int i4 = 0; i4 < MB - 4; ++i4) xl[i4 * Zc + z] = lrow[(KB + 4 + i4 - pc) * Zc + z];
+        for (int i4 = 0; i4 < MB - 4; ++i4) {
+            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            if constexpr (XL_LDS) at(XL_B + i4 * kCS * TS + tzb) = v;
+            hdx_prev |= (uint64_t)(v < T(0)) << i4;
+        }
     }
-    if (z == 0 && valid) flag[cbl] = 0;
+    if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
     bool active = valid;
     __syncthreads();
 
-    // zv / shv are re-materialised opaque each iteration: otherwise LICM hoists the ~300
-    // loop-invariant column addresses (z + V) mod Zc out of the iteration loop into VGPRs.
-    int zv = z;
-    const uint16_t* shv = sh;
-    auto lds_col = [&](int j, int s) -> int {   // LDS index of column j*Zc + (z+s)%Zc
-        int zz = zv + s;
-        zz = zz >= Zc ? zz - Zc : zz;
-        return j * Zc + zz;
-    };
+    int zv = z, ziv = zi;   // made opaque per iteration (see below)
+    // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
+    auto rot = [&](int s) -> int { return tzb + s * TS - (zv >= Zc - s ? ZcT : 0); };
 
     int it = 0;
     for (; it < L; ++it) {
+        // zv / ziv are re-materialised opaque each iteration: otherwise LICM hoists the ~300
+        // loop-invariant column addresses (z + V) mod Zc out of the loop into VGPRs/SGPRs.
         zv = z;
-        shv = sh;
+        ziv = zi;
         asm volatile("" : "+v"(zv));
-        asm volatile("" : "+s"(shv));
-        bool fail = false, flip = false;
-        uint64_t hdx = 0;   // flooding: hard decisions of the extension columns at pass start
-        sfor<0, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i];
-            constexpr int d = P::RS[i + 1] - e0;
+        asm volatile("" : "+s"(ziv));
+        bool fail = false;
+        uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
+        sfor<0, kGroups<BG>.n>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
             if (active) {
-                const T mA = sA[i], mB = sB[i];
-                const uint32_t pk = sP[i];
-                T q[d];
-                T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-                uint32_t idx = 0, negs = 0, hdo = 0;
-                bool par = false;
-                sfor<0, d>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int j = P::COL[e0 + k];
-                    const T rold = decomp(mA, mB, pk, k);
-                    T a_old, qq;
-                    if constexpr (j < KC) {
-                        a_old = app[lds_col(j, shv[e0 + k])];
-                        qq = a_old - rold;
-                    } else {
-                        a_old = llrx(i - 4) + rold;   // APP of a degree-1 column
-                        if constexpr (LAYERED) qq = llrx(i - 4);
-                        else qq = a_old - rold;
-                        if constexpr (!LAYERED) hdx |= (uint64_t)(a_old < T(0)) << (i - 4);
-                    }
-                    const bool h = a_old < T(0);
-                    par ^= h;
-                    hdo |= (uint32_t)h << k;
-                    q[k] = qq;
-                    const T a = qq < T(0) ? -qq : qq;
-                    const bool lt = a < min1;
-                    min2 = lt ? min1 : (a < min2 ? a : min2);
-                    idx = lt ? (uint32_t)k : idx;
-                    min1 = lt ? a : min1;
-                    negs |= (uint32_t)(qq < T(0)) << k;
-                });
-                fail |= par;
-                const uint32_t s = __popc(negs) & 1u;
-                const T x1 = min1 - beta, x2 = min2 - beta;
-                const T nA = alpha * (x1 > T(0) ? x1 : T(0));
-                const T nB = alpha * (x2 > T(0) ? x2 : T(0));
-                const uint32_t npk = (negs ^ (s ? ((1u << d) - 1u) : 0u)) | (idx << 24);
-                sA[i] = nA;
-                sB[i] = nB;
-                sP[i] = npk;
-                sfor<0, d>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int j = P::COL[e0 + k];
-                    const T r = decomp(nA, nB, npk, k);
-                    if constexpr (LAYERED) {
-                        T nv;
+                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    constexpr int e0 = P::RS[i];
+                    constexpr int d = P::RS[i + 1] - e0;
+                    const T mA = sA[i], mB = sB[i];
+                    const uint32_t pk = sP[i];
+                    const uint32_t idxo = pk >> 24;
+                    T q[d];
+                    int rb[d];
+                    T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+                    uint32_t sx = 0, idx = 0, negs = 0;
+                    bool par = false;
+                    // ---- pass 1: variable-to-check messages q, two-min, sign product
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        const T rold = decomp(mA, mB, pk, idxo, k);
+                        T qq;
                         if constexpr (j < KC) {
-                            nv = q[k] + r;
-                            app[lds_col(j, shv[e0 + k])] = nv;
+                            rb[k] = rot(shift_of<BG>(ziv, e0 + k));
+                            const T a = at(j * kCS * TS + rb[k]);
+                            qq = a - rold;
+                            if constexpr (!LAYERED) par ^= a < T(0);
+                        } else if constexpr (LAYERED) {
+                            qq = llrx(i - 4);   // degree-1 column: q is the channel LLR itself
                         } else {
-                            nv = llrx(i - 4) + r;
+                            const T a = llrx(i - 4) + rold;   // LQ of a degree-1 column
+                            qq = a - rold;
+                            const bool h = a < T(0);
+                            par ^= h;
+                            hdx |= (uint64_t)h << (i - 4);
                         }
-                        flip |= (nv < T(0)) != (bool)((hdo >> k) & 1u);
-                    } else {
-                        if constexpr (j < KC) {
-                            const int a = lds_col(j, shv[e0 + k]);
-                            acc[a] = acc[a] + r;   // row-ascending accumulation (:126)
+                        q[k] = qq;
+                        const T aq = fabs(qq);
+                        if constexpr (!LAYERED) {
+                            idx = aq < min1 ? (uint32_t)k : idx;
+                            negs |= (FT<T>::sbits(qq) >> 31) << k;
                         }
-                    }
+                        min2 = FT<T>::med3(min1, min2, aq);
+                        min1 = fmin(min1, aq);
+                        sx ^= FT<T>::sbits(qq);
+                    });
+                    fail |= par;
+                    const T x1 = min1 - beta, x2 = min2 - beta;
+                    const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
+                    const T nB = alpha * (x2 > T(0) ? x2 : T(0));
+                    // ---- pass 2: check-to-variable messages r = sign * (k == argmin ? nB : nA)
+                    uint32_t signs = 0, idxn = 0;
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        T r;
+                        if constexpr (LAYERED) {
+                            const T aq = fabs(q[k]);
+                            const bool isMin = aq == min1;   // ties: nB == nA, either is right
+                            idxn = isMin ? (uint32_t)k : idxn;
+                            const uint32_t sb = FT<T>::sbits(q[k]) ^ sx;
+                            r = FT<T>::xsign(isMin ? nB : nA, sb);
+                            signs |= (sb >> 31) << k;
+                            if constexpr (j < KC) {
+                                at(j * kCS * TS + rb[k]) = q[k] + r;
+                            } else {
+                                hdx |= (uint64_t)(llrx(i - 4) + r < T(0)) << (i - 4);
+                            }
+                        } else {
+                            const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
+                            r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
+                            if constexpr (j < KC) {
+                                T& a = at(ACC_B + j * kCS * TS + rb[k]);
+                                a = a + r;   // row-ascending accumulation (:126)
+                            }
+                        }
+                    });
+                    sA[i] = nA;
+                    sB[i] = nB;
+                    if constexpr (LAYERED) sP[i] = signs | (idxn << 24);
+                    else sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
                 });
             }
             __syncthreads();
         });
-        if (active && (fail || flip)) flag[cl] = 1;
-        __syncthreads();
-        const bool conv = active && flag[cl] == 0;
-        if (conv) {
-            // early exit: ck = hard decision (APP < 0) of the state the check passed on
-            for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(app[j * Zc + z] < T(0));
-            sfor<4, MB>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                int8_t h;
-                if constexpr (LAYERED) {
-                    constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
-                    h = (int8_t)(llrx(i - 4) + decomp(sA[i], sB[i], sP[i], dl) < T(0));
-                } else {
-                    h = (int8_t)((hdx >> (i - 4)) & 1u);   // LQ of the checked pass (state moved on)
+
+        if constexpr (!LAYERED) {
+            // ---- reference order: the syndrome of LQ at the start of the pass decides (:107-114)
+            if (active && fail) flagA[cl] = 1;
+            __syncthreads();
+            const bool conv = active && flagA[cl] == 0;
+            if (conv) {
+                for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(own(j) < T(0));
+                for (int i4 = 0; i4 < MB - 4; ++i4)
+                    crow[(KB + 4 + i4) * Zc + z] = (int8_t)((hdx >> i4) & 1u);
+                if (z == 0) status[out] = 1, iters[out] = it;
+                active = false;
+            } else if (active) {
+                for (int j = 0; j < KC; ++j) {
+                    T& acc = at(ACC_B + j * kCS * TS + tzb);
+                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+                    own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
+                    acc = T(0);
                 }
-                crow[(KB + i) * Zc + z] = h;
-            });
-            if (z == 0) {
-                status[out] = 1;
-                iters[out] = LAYERED ? it + 1 : it;
             }
-            active = false;
-        } else if (active && !LAYERED) {
-            for (int j = 0; j < KC; ++j) {
-                const int a = j * Zc + z;
-                const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
-                app[a] = lf + acc[a];   // LQ = LLR + sum Lr (:126)
-                acc[a] = T(0);
+        } else {
+            // ---- layered stopping rule: no hard decision changed over the iteration, then an
+            //      exact syndrome check of those decisions (oracle.decode_layered)
+            uint32_t hdc = 0;
+            if (active)
+                for (int j = 0; j < KC; ++j) hdc |= (uint32_t)(own(j) < T(0)) << j;
+            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;
+            hdc_prev = hdc;
+            hdx_prev = hdx;
+            __syncthreads();
+            const bool cand = active && flagA[cl] == 0;
+            if (__syncthreads_or(cand)) {
+                if (cand) {
+                    bool sf = false;
+                    sfor<0, MB>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        constexpr int e0 = P::RS[i];
+                        constexpr int d = P::RS[i + 1] - e0;
+                        bool par = false;
+                        sfor<0, d>([&](auto kc) {
+                            constexpr int k = decltype(kc)::value;
+                            constexpr int j = P::COL[e0 + k];
+                            if constexpr (j < KC)
+                                par ^= at(j * kCS * TS + rot(shift_of<BG>(ziv, e0 + k))) < T(0);
+                            else
+                                par ^= (bool)((hdx >> (i - 4)) & 1u);
+                        });
+                        sf |= par;
+                    });
+                    if (sf) flagB[cl] = 1;
+                }
+                __syncthreads();
+                if (cand && flagB[cl] == 0) {
+                    for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)((hdc >> j) & 1u);
+                    for (int i4 = 0; i4 < MB - 4; ++i4)
+                        crow[(KB + 4 + i4) * Zc + z] = (int8_t)((hdx >> i4) & 1u);
+                    if (z == 0) status[out] = 1, iters[out] = it + 1;
+                    active = false;
+                }
             }
         }
         __syncthreads();
-        if (z == 0 && valid) flag[cl] = 0;
+        if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
         if (!__syncthreads_or(active)) break;
     }
 
@@ -576,25 +676,25 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
                 T a;
-                if constexpr (j < KC) a = app[lds_col(j, shv[e0 + k])];
-                else a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], k);
+                if constexpr (j < KC) a = at(j * kCS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                else a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
                 par ^= (a <= T(0));
             });
             fail |= par;
         });
-        if (fail) flag[cl] = 1;
+        if (fail) flagA[cl] = 1;
     }
     __syncthreads();
     if (active) {
-        for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(app[j * Zc + z] <= T(0));
+        for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(own(j) <= T(0));
         sfor<4, MB>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;
-            const T a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], dl);
+            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+            const T a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, dl);
             crow[(KB + i) * Zc + z] = (int8_t)(a <= T(0));
         });
         if (z == 0) {
-            status[out] = flag[cl] == 0;
+            status[out] = flagA[cl] == 0;
             iters[out] = L;
         }
     }
@@ -627,9 +727,8 @@ int check_hip(hipError_t e, const char* what) {
 inline int dec_G(int Zc) { return Zc >= kDecThreads ? 1 : kDecThreads / Zc; }
 
 template <int BG, typename T, bool LAYERED>
-size_t dec_lds_bytes(int Zc, int G) {
-    const size_t xl = sizeof(T) == 4 ? (size_t)G * (BGT<BG>::MB - 4) * Zc * sizeof(T) : 0;
-    return (size_t)G * BGT<BG>::KC * Zc * sizeof(T) * (LAYERED ? 1 : 2) + xl + (size_t)G * sizeof(int);
+size_t dec_lds_bytes() {
+    return dec_lds_bytes_t<T, LAYERED>(BGT<BG>::MB, BGT<BG>::KC);
 }
 
 template <int BG, typename T, bool LAYERED>
@@ -637,7 +736,7 @@ int launch_dec(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
                int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
     auto kern = ldpc_dec_kernel<BG, T, LAYERED>;
     const int G = dec_G(Zc);
-    const size_t lds = dec_lds_bytes<BG, T, LAYERED>(Zc, G);
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     const int threads = ((G * Zc + 63) / 64) * 64;
     const int grid = (B + G - 1) / G;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -652,7 +751,7 @@ int launch_dec_mixed(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
                      const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                      int pc, hipStream_t st) {
     auto kern = ldpc_dec_kernel<BG, T, LAYERED>;
-    const size_t lds = dec_lds_bytes<BG, T, LAYERED>(kDecThreads, 1) + kDecThreads * sizeof(int);
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kDecThreads), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
