@@ -1,0 +1,50 @@
+"""The drop-in modules expose the reference's call surface: same function names, parameter
+names, order and defaults.  Compared against the reference's source via `inspect` when the
+reference is present (build container); skipped elsewhere (the GPU box never has it)."""
+import ast
+import inspect
+import os
+
+import pytest
+
+REF = "/root/reference/py5gphy"
+
+PAIRS = [
+    ("ldpc/nr_ldpc_encode.py", "python_5gtoolbox_amd.nr_ldpc_encode", ["encode_ldpc"]),
+    ("ldpc/nr_ldpc_decode.py", "python_5gtoolbox_amd.nr_ldpc_decode",
+     ["nr_decode_ldpc", "decode_ldpc", "for_test_5g_ldpc_encoder"]),
+    ("ldpc/ldpc_info.py", "python_5gtoolbox_amd.ldpc_info",
+     ["get_cbs_info", "find_iLS", "getH", "gen_ldpc_para"]),
+    ("ldpc/nr_ldpc_cbsegment.py", "python_5gtoolbox_amd.nr_ldpc_cbsegment", ["ldpc_cbsegment"]),
+    ("ldpc/nr_ldpc_ratematch.py", "python_5gtoolbox_amd.nr_ldpc_ratematch",
+     ["get_Er_ldpc", "get_k0", "ratematch_ldpc"]),
+    ("ldpc/nr_ldpc_raterecover.py", "python_5gtoolbox_amd.nr_ldpc_raterecover", ["raterecover_ldpc"]),
+    ("crc/crc.py", "python_5gtoolbox_amd.crc", ["nr_crc_encode", "nr_crc_decode"]),
+]
+
+
+def _ref_signatures(path):
+    """(arg names, defaults) of each top-level def, parsed from the reference source text."""
+    tree = ast.parse(open(os.path.join(REF, path)).read())
+    out = {}
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef):
+            names = [a.arg for a in node.args.args]
+            defaults = [ast.literal_eval(d) for d in node.args.defaults]
+            out[node.name] = (names, defaults)
+    return out
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference not present")
+@pytest.mark.parametrize("path,mod,funcs", PAIRS)
+def test_signatures_match_reference(path, mod, funcs):
+    import importlib
+    m = importlib.import_module(mod)
+    ref = _ref_signatures(path)
+    for f in funcs:
+        sig = inspect.signature(getattr(m, f))
+        names = list(sig.parameters)
+        defaults = [p.default for p in sig.parameters.values() if p.default is not p.empty]
+        rnames, rdefaults = ref[f]
+        assert names == rnames, (f, names, rnames)
+        assert defaults == rdefaults, (f, defaults, rdefaults)

@@ -1,0 +1,81 @@
+"""CPU (gloo, world_size 2) tests of the multi-GPU sharding/gather logic.
+
+The per-rank decode here is the oracle injected as `decode_fn` (test infrastructure); on the
+GPU box the same code path runs the HIP decoder over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from python_5gtoolbox_amd.shard import shard_bounds, shard_round_robin
+
+
+def test_shard_bounds_cover_exactly():
+    for n in [0, 1, 7, 4096, 4097]:
+        for w in [1, 2, 3, 8]:
+            got = [shard_bounds(n, r, w) for r in range(w)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
+            sizes = [hi - lo for lo, hi in got]
+            assert max(sizes) - min(sizes) <= 1
+    assert shard_round_robin(10, 1, 4) == [1, 5, 9]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import ldpc_oracle as O
+        from python_5gtoolbox_amd.shard import decode_codeblocks_sharded, decode_tbs_sharded
+        bg, Zc, B = 2, 12, 11
+        rng = np.random.default_rng(5)           # same data on every rank (the "full batch")
+        ck = rng.integers(0, 2, (B, 10 * Zc)).astype(np.int8)
+        llr = O.bpsk_awgn_llr(O.encode(ck, bg), 1.0, rng).astype(np.float32)
+
+        def dec(x):
+            c, s, i = O.decode_layered(x.numpy(), Zc, bg, 8, 0.75, 0.0)
+            return torch.from_numpy(c), torch.from_numpy(s), torch.from_numpy(i)
+
+        res = decode_codeblocks_sharded(torch.from_numpy(llr), Zc, bg, 8, 0.75, 0.0,
+                                        decode_fn=dec)
+        tb = decode_tbs_sharded(list(range(5)), lambda x: (x % 2 == 0, [x, rank]))
+        if rank == 0:
+            rc, rs, ri = O.decode_layered(llr, Zc, bg, 8, 0.75, 0.0)
+            ok = (np.array_equal(res[0].numpy(), rc[:, :10 * Zc])
+                  and np.array_equal(res[1].numpy().astype(bool), rs)
+                  and np.array_equal(res[2].numpy(), ri)
+                  and [t[0] for t in tb] == [True, False, True, False, True]
+                  and [int(t[1][1]) for t in tb] == [i % world for i in range(5)])
+            q.put(ok)
+        else:
+            q.put(res is None and tb is None)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_decode_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(results), results
