@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libldpc5g.so")
+LIB_PATH = os.environ.get("LDPC5G_LIB") or os.path.join(HERE, "libldpc5g.so")
 
 F64, F32 = 0, 1
 FLOODING, LAYERED = 0, 1

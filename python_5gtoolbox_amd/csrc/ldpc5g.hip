@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -339,6 +340,181 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
     }
 }
 
+// Fast encoder: Zc % 16 == 0 and 16-B aligned rows (every BG1/BG2 Zc >= 16 that is a multiple
+// of 16, including the Zc=384 hot path).  Same arithmetic as ldpc_enc_kernel; the differences are
+// where bytes go: systematic bytes are stored straight from the load registers, every parity
+// row-word (32 bits of one base row) is expanded and stored straight to dn as 32 (or 16) bytes,
+// and the p1..p4 recursion runs inside wave 0 with wave-level syncs (no parity bit array, no LDS
+// atomics, 4 workgroup barriers instead of 9).
+struct EncFastLayout {
+    int K, N, W, DW, KW, words;
+};
+template <int BG>
+__host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
+    using P = BGT<BG>;
+    EncFastLayout L;
+    L.K = P::KB * Zc;
+    L.N = (P::NB - 2) * Zc;
+    L.W = (Zc + 31) >> 5;
+    L.DW = 2 * L.W + 2;
+    L.KW = (L.K + 31) >> 5;
+    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2]
+    L.words = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + 2;
+    return L;
+}
+template <int BG>
+inline size_t enc_fast_lds_bytes(int Zc) {
+    return (size_t)enc_fast_layout<BG>(Zc).words * 4;
+}
+
+// 32 parity bits -> 32 int8 bytes (nbits = 32 or 16) at a 16-B aligned address
+__device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits) {
+    uint4 a = make_uint4(expand4(bits & 15u), expand4((bits >> 4) & 15u), expand4((bits >> 8) & 15u),
+                         expand4((bits >> 12) & 15u));
+    *(uint4*)dst = a;
+    if (nbits > 16) {
+        uint4 b = make_uint4(expand4((bits >> 16) & 15u), expand4((bits >> 20) & 15u),
+                             expand4((bits >> 24) & 15u), expand4(bits >> 28));
+        *(uint4*)(dst + 16) = b;
+    }
+}
+
+template <int BG>
+__global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
+                                                            int8_t* __restrict__ dn, int B, int Zc,
+                                                            int zi, int64_t ldk, int64_t ldn) {
+    using P = BGT<BG>;
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int t = threadIdx.x;
+    const int NT = blockDim.x;
+    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
+    const int K = Ly.K, W = Ly.W, DW = Ly.DW, KW = Ly.KW;
+    const int twoZ = 2 * Zc;
+    const int S = K - twoZ;
+    extern __shared__ __align__(16) uint32_t sm[];
+    uint32_t* ib = sm;
+    uint32_t* X = ib + KW + 2;
+    uint32_t* lam = X + P::KC * DW;
+    uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
+    const int8_t* src = ck + (int64_t)b * ldk;
+    int8_t* dst = dn + (int64_t)b * ldn;
+
+    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn
+    for (int wi = t; wi < KW; wi += NT) {
+        const int base = wi * 32;   // K = Kb*Zc is a multiple of 32 when Zc % 16 == 0
+        uint32_t bits = 0;
+        if (base + 32 <= K) {
+            int4 v[2];
+            v[0] = *(const int4*)(src + base);
+            v[1] = *(const int4*)(src + base + 16);
+            if (base >= twoZ) {   // 2Zc and K are multiples of 32 here
+                *(int4*)(dst + base - twoZ) = v[0];
+                *(int4*)(dst + base - twoZ + 16) = v[1];
+            }
+            const uint32_t* d = (const uint32_t*)v;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t x = d[q];
+                // per byte: LSB, minus fillers (0xff) at positions >= 2Zc
+                uint32_t lsb = x & 0x01010101u;
+                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                                     (x >> 6) & (x >> 7)) & 0x01010101u;   // byte == 0xff
+                if (base + 4 * q >= twoZ) lsb &= ~ff;
+                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+            }
+        } else {   // (unreachable for Kb*Zc % 32 == 0; kept for safety)
+            int4 v0 = *(const int4*)(src + base);
+            if (base >= twoZ) *(int4*)(dst + base - twoZ) = v0;
+            const uint32_t* d = (const uint32_t*)&v0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = d[q];
+                uint32_t lsb = x & 0x01010101u;
+                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                                     (x >> 6) & (x >> 7)) & 0x01010101u;
+                if (base + 4 * q >= twoZ) lsb &= ~ff;
+                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+            }
+        }
+        ib[wi] = bits;
+    }
+    if (t < 2) ib[KW + t] = 0;
+    __syncthreads();
+
+    // ---- 2. periodic extensions of the information columns
+    for (int task = t; task < P::KB * DW; task += NT) {
+        int j = task / DW, q = task - j * DW;
+        X[j * DW + q] = fetch_rot32(ib, j * Zc, Zc, mod_zc(32 * q, Zc));
+    }
+    __syncthreads();
+
+    // ---- 3+4. lambda and the double-diagonal recursion, all inside wave 0
+    constexpr int eS = (BG == 1) ? edge_of<BG>(1, 22) : edge_of<BG>(2, 10);
+    constexpr int eA = edge_of<BG>(0, P::KB);
+    constexpr int eC = edge_of<BG>(3, P::KB);
+    constexpr int eD = (BG == 1) ? edge_of<BG>(2, 25) : edge_of<BG>(1, 11);
+    uint32_t* p1 = pv;
+    uint32_t* p2 = pv + W;
+    uint32_t* p3 = pv + 2 * W;
+    uint32_t* p4 = pv + 3 * W;
+    uint32_t* L2 = pv + 4 * W;
+    if (t < 64) {
+        for (int task = t; task < 4 * W; task += 64) {
+            int i = task / W, w = task - i * W;
+            uint32_t acc = 0;
+            for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+                int j = col_d<BG>(e);
+                if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+            }
+            lam[i * W + w] = acc;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) L2[w] = lam[w] ^ lam[W + w] ^ lam[2 * W + w] ^ lam[3 * W + w];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int s1 = shift_of<BG>(zi, eS);
+        for (int w = t; w < W; w += 64)
+            p1[w] = fetch_rot32(L2, 0, Zc, mod_zc(mod_zc(32 * w, Zc) + Zc - s1, Zc));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) {
+            p2[w] = lam[w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eA), Zc));
+            p4[w] = lam[3 * W + w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eC), Zc));
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) {
+            if constexpr (BG == 1) p3[w] = lam[2 * W + w] ^ fetch_rot32(p4, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+            else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+        }
+    }
+    __syncthreads();
+
+    // ---- 5. extensions of the 4 core parity columns; core parity bytes straight to dn
+    for (int task = t; task < 4 * DW; task += NT) {
+        int k = task / DW, q = task - k * DW;
+        X[(P::KB + k) * DW + q] = fetch_rot32(pv + k * W, 0, Zc, mod_zc(32 * q, Zc));
+    }
+    for (int task = t; task < 4 * W; task += NT) {
+        int k = task / W, w = task - k * W;
+        store_bits(dst + S + k * Zc + 32 * w, pv[k * W + w], min(32, Zc - 32 * w));
+    }
+    __syncthreads();
+
+    // ---- 6. extension parity rows, each row-word stored straight to dn
+    for (int task = t; task < (P::MB - 4) * W; task += NT) {
+        int i = 4 + task / W, w = task % W;
+        uint32_t acc = 0;
+        for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+            int j = col_d<BG>(e);
+            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+        }
+        store_bits(dst + S + i * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+    }
+}
+
 // ================================================================================== DECODER
 template <typename T>
 struct FT;
@@ -403,6 +579,25 @@ struct RowGroups {
 template <int BG>
 constexpr RowGroups<BG> kGroups{};
 
+// Packed shift words (2 edges per word) spanned by the edges of row group g.
+template <int BG>
+constexpr int group_w0(int g) { return BGT<BG>::RS[kGroups<BG>.start[g]] >> 1; }
+template <int BG>
+constexpr int group_nw(int g) {
+    return ((BGT<BG>::RS[kGroups<BG>.start[g + 1]] - 1) >> 1) - group_w0<BG>(g) + 1;
+}
+template <int BG>
+constexpr int max_group_nw() {
+    int m = 0;
+    for (int g = 0; g < kGroups<BG>.n; ++g) m = m > group_nw<BG>(g) ? m : group_nw<BG>(g);
+    return m;
+}
+template <int BG>
+__device__ __forceinline__ uint32_t shift_word(int zi, int w) {
+    if constexpr (BG == 1) return kBG1ShiftMod[zi][w];
+    else return kBG2ShiftMod[zi][w];
+}
+
 struct DecWork {     // one workgroup of the mixed-Zc path
     int32_t zi, Zc, G, first;
 };
@@ -465,6 +660,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     const int cl = valid ? cbl : 0;
     const int tzb = (cl * Zc + z) * TS;   // byte offset of this thread's own column entry
     const int ZcT = Zc * TS;
+    int zv = z, ziv = zi;   // made opaque per iteration (see the iteration loop)
     int* flagA = (int*)(smem + FLAG_B);
     int* flagB = flagA + kCS;
     auto at = [&](int byte) -> T& { return *(T*)(smem + byte); };
@@ -472,7 +668,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
     auto llrx = [&](int i4) -> T {
         if constexpr (XL_LDS) return at(XL_B + i4 * kCS * TS + tzb);
-        else return lrow[(KB + 4 + i4 - pc) * Zc + z];
+        else return lrow[(KB + 4 + i4 - pc) * Zc + zv];
     };
 
     // per-thread state of rows (i, z), i = 0..MB-1
@@ -500,7 +696,6 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     bool active = valid;
     __syncthreads();
 
-    int zv = z, ziv = zi;   // made opaque per iteration (see below)
     // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
     auto rot = [&](int s) -> int { return tzb + s * TS - (zv >= Zc - s ? ZcT : 0); };
 
@@ -514,8 +709,27 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         asm volatile("" : "+s"(ziv));
         bool fail = false;
         uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
+        // the next row group's packed shift words are loaded (scalar, wave-uniform) before the
+        // barrier that precedes the group, so their latency hides behind it
+        constexpr int NPW = max_group_nw<BG>();
+        uint32_t nsw[NPW];
+        auto prefetch = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            sfor<0, group_nw<BG>(g)>([&](auto wc) {
+                constexpr int w = decltype(wc)::value;
+                nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
+            });
+        };
+        prefetch(std::integral_constant<int, 0>{});
         sfor<0, kGroups<BG>.n>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
+            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
+            auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
+                return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+            };
             if (active) {
                 sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
                     constexpr int i = decltype(ic)::value;
@@ -536,7 +750,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                         const T rold = decomp(mA, mB, pk, idxo, k);
                         T qq;
                         if constexpr (j < KC) {
-                            rb[k] = rot(shift_of<BG>(ziv, e0 + k));
+                            rb[k] = rot(gshift(e0 + k));
                             const T a = at(j * kCS * TS + rb[k]);
                             qq = a - rold;
                             if constexpr (!LAYERED) par ^= a < T(0);
@@ -596,6 +810,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                     else sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
                 });
             }
+            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
             __syncthreads();
         });
 
@@ -605,15 +820,15 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
             __syncthreads();
             const bool conv = active && flagA[cl] == 0;
             if (conv) {
-                for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(own(j) < T(0));
+                for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
                 for (int i4 = 0; i4 < MB - 4; ++i4)
-                    crow[(KB + 4 + i4) * Zc + z] = (int8_t)((hdx >> i4) & 1u);
+                    crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
                 if (z == 0) status[out] = 1, iters[out] = it;
                 active = false;
             } else if (active) {
                 for (int j = 0; j < KC; ++j) {
                     T& acc = at(ACC_B + j * kCS * TS + tzb);
-                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
                     own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
                     acc = T(0);
                 }
@@ -651,9 +866,9 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                 }
                 __syncthreads();
                 if (cand && flagB[cl] == 0) {
-                    for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)((hdc >> j) & 1u);
+                    for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)((hdc >> j) & 1u);
                     for (int i4 = 0; i4 < MB - 4; ++i4)
-                        crow[(KB + 4 + i4) * Zc + z] = (int8_t)((hdx >> i4) & 1u);
+                        crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
                     if (z == 0) status[out] = 1, iters[out] = it + 1;
                     active = false;
                 }
@@ -665,6 +880,8 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     }
 
     // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
+    zv = z;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
     if (active) {
         bool fail = false;
         sfor<0, MB>([&](auto ic) {
@@ -686,12 +903,12 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     }
     __syncthreads();
     if (active) {
-        for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(own(j) <= T(0));
+        for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
         sfor<4, MB>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
             const T a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, dl);
-            crow[(KB + i) * Zc + z] = (int8_t)(a <= T(0));
+            crow[(KB + i) * Zc + zv] = (int8_t)(a <= T(0));
         });
         if (z == 0) {
             status[out] = flagA[cl] == 0;
@@ -791,6 +1008,23 @@ int ldpc5g_encode(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t 
     if (B == 0) return LDPC5G_OK;
     if (!ck || !dn) return fail(LDPC5G_ESIZE, "null buffer");
     hipStream_t st = (hipStream_t)stream;
+    const bool fast = (Zc % 16) == 0 && (ldk % 16) == 0 && (ldn % 16) == 0 &&
+                      (((uintptr_t)ck) & 15) == 0 && (((uintptr_t)dn) & 15) == 0;
+    if (fast) {
+        static const int nt = [] {
+            const char* e = getenv("LDPC5G_ENC_THREADS");
+            int v = e ? atoi(e) : 64;
+            return (v == 64 || v == 128 || v == 256) ? v : 64;
+        }();
+        if (bgn == 1) {
+            size_t lds = enc_fast_lds_bytes<1>(Zc);
+            hipLaunchKernelGGL(ldpc_enc_fast_kernel<1>, dim3(B), dim3(nt), lds, st, ck, dn, B, Zc, zi, ldk, ldn);
+        } else {
+            size_t lds = enc_fast_lds_bytes<2>(Zc);
+            hipLaunchKernelGGL(ldpc_enc_fast_kernel<2>, dim3(B), dim3(nt), lds, st, ck, dn, B, Zc, zi, ldk, ldn);
+        }
+        return check_hip(hipGetLastError(), "ldpc_enc_fast_kernel launch");
+    }
     if (bgn == 1) {
         size_t lds = enc_lds_bytes<1>(Zc);
         hipLaunchKernelGGL(ldpc_enc_kernel<1>, dim3(B), dim3(256), lds, st, ck, dn, B, Zc, zi, ldk, ldn);

@@ -1,0 +1,58 @@
+"""Throughput probes (development tool, not the bench contract): time the encoder / decoders
+over several batch sizes with HIP events.
+
+    python tools/probe.py encode 1024 4096 16384 65536
+    python tools/probe.py layered 1024 4096 8192
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from python_5gtoolbox_amd import nr_ldpc_decode as D, nr_ldpc_encode as E  # noqa: E402
+
+ZC, K, N, NF = 384, 22 * 384, 66 * 384, 68 * 384
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    what = sys.argv[1]
+    sizes = [int(x) for x in sys.argv[2:]] or [4096]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    for B in sizes:
+        ck = torch.randint(0, 2, (B, K), dtype=torch.int8, device="cuda", generator=g)
+        if what == "encode":
+            dn = torch.empty((B, N), dtype=torch.int8, device="cuda")
+            ms = timeit(lambda: E.encode_ldpc_batch(ck, 1, out=dn), 50)
+            print(f"encode B={B}: {ms * 1e3:.1f} us  {B / ms / 1e3:.1f} M CB/s  "
+                  f"{B * (K + N) / ms / 1e6:.0f} GB/s")
+        else:
+            dn = E.encode_ldpc_batch(ck, 1)
+            sigma = 10 ** (3.0 / 20)
+            llr = (2 * ((1 - 2 * dn.float()) + sigma * torch.randn(dn.shape, device="cuda",
+                                                                     generator=g)) / sigma ** 2)
+            out = (torch.empty((B, NF), dtype=torch.int8, device="cuda"),
+                   torch.empty((B,), dtype=torch.uint8, device="cuda"),
+                   torch.empty((B,), dtype=torch.int32, device="cuda"))
+            ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, 1, 8, "min-sum", 0.75, 0.0, what,
+                                                       out=out), 5)
+            print(f"{what} B={B}: {ms:.3f} ms  {B / ms / 1e3:.1f} k CB/s  iters "
+                  f"{out[2].float().mean().item():.2f}")
+
+
+if __name__ == "__main__":
+    main()
