@@ -73,6 +73,22 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
                      double alpha, double beta, int32_t schedule, int32_t flags, int64_t ldl,
                      int64_t ldc, void* stream);
 
+/* Hard-decision bit flipping (algo='BF')  <- py5gphy/ldpc/ldpc_decoder_bit_flipping.py:5-73
+ * reached through nr_decode_ldpc(..., algo='BF') (nr_ldpc_decode.py:65-67).  Same buffers as
+ * ldpc5g_decode_ms; ck holds the 0/1 decisions (the reference returns them as float64), status
+ * is 0 after L iterations without a zero syndrome (the reference checks only at loop start). */
+int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
+                     int32_t* iters, int32_t B, int32_t bgn, int32_t Zc, int32_t L,
+                     int32_t flags, int64_t ldl, int64_t ldc, void* stream);
+
+/* Float64 sum-product, flooding (algo='BP')  <- nr_ldpc_decode.py:51-143 + _BP_process :145-176.
+ * Per-edge messages do not compress: the caller provides a float64 device scratch of
+ * ldpc5g_bp_scratch_elems(B, bgn, Zc) elements (-1 on bad arguments). */
+int64_t ldpc5g_bp_scratch_elems(int32_t B, int32_t bgn, int32_t Zc);
+int ldpc5g_decode_bp(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                     double* scratch, int64_t scratch_elems, int32_t B, int32_t bgn, int32_t Zc,
+                     int32_t L, int32_t flags, int64_t ldl, int64_t ldc, void* stream);
+
 /* One codeblock of a mixed batch: base graph, lifting size, element offsets of its LLR row
  * (into llr_base, in elements) and of its ck row (into ck_base, in bytes). */
 typedef struct {

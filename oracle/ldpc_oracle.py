@@ -14,7 +14,9 @@ Contents (reference file:line each restates):
   graph / getH ................... py5gphy/ldpc/ldpc_info.py:99-139 (edge-list form, no dense H)
   encode ......................... py5gphy/ldpc/nr_ldpc_encode.py:8-50, :52-115 (optimised A/B/C path)
   decode_flooding ................ py5gphy/ldpc/nr_ldpc_decode.py:11-49, :51-143, :178-227
-  decode_layered ................. (no reference: the build's layered perf schedule, DESIGN.md §4.3)
+  decode_layered ................. (no reference: the build's layered perf schedule, DESIGN.md §4.2)
+  decode_bf ...................... py5gphy/ldpc/ldpc_decoder_bit_flipping.py:5-73
+  decode_bp ...................... py5gphy/ldpc/nr_ldpc_decode.py:51-143, :145-176
   crc_encode / crc_decode ........ py5gphy/crc/crc.py:4-88
   get_Er / get_k0 / ratematch / raterecover  py5gphy/ldpc/nr_ldpc_ratematch.py:5-97,
                                               py5gphy/ldpc/nr_ldpc_raterecover.py:6-65
@@ -353,6 +355,121 @@ def decode_layered(llr, Zc, bgn, L, alpha=1.0, beta=0.0):
         f = _row_hd_fail(hd, g)
         ck[rem] = hd[rem]
         status[rem] = ~f[rem]
+    return ck, status, iters
+
+
+def decode_bf(llr, Zc, bgn, L, full=False):
+    """nr_decode_ldpc(..., algo='BF') -> ldpc_decoder_BF (ldpc_decoder_bit_flipping.py:5-73),
+    batched.  Returns ck (B, Nf) int8 (the reference returns the same 0/1 values as float64),
+    status (B,) bool, iters (B,) int32.
+      ck = LLR<0 (LLR==0 stays 0)                            (:41-43)
+      for it < L: S = H ck mod 2; if S == 0 -> (ck, True)   (:47-56)
+                  En = (2S-1) H; flip every bit with En == max(En)   (:61-70)
+      (ck, False)                                            (:72-73)"""
+    llr = np.atleast_2d(np.asarray(llr))
+    g = graph(bgn, Zc)
+    B = llr.shape[0]
+    Lfull = llr if full else np.concatenate([np.zeros((B, 2 * Zc)), llr], axis=1)
+    assert Lfull.shape[1] == g.Nf
+    ck = (Lfull < 0).astype(np.uint8)
+    done = np.zeros(B, bool)
+    status = np.zeros(B, bool)
+    iters = np.full(B, L, np.int32)
+    for it in range(L):
+        S = np.zeros((B, g.Mb, Zc), np.int64)
+        for i in range(g.Mb):
+            S[:, i] = np.bitwise_xor.reduce(ck[:, g.rows_cols(i)], axis=1)
+        ok = ~S.reshape(B, -1).any(axis=1) & ~done
+        status[ok] = True
+        iters[ok] = it
+        done |= ok
+        if done.all():
+            break
+        En = np.zeros((B, g.Nf), np.int64)
+        for b in range(len(g.bi)):   # column ecol[b, m] meets row bi*Zc + m
+            En[:, g.ecol[b]] += 2 * S[:, g.bi[b]] - 1
+        flip = En == En.max(axis=1, keepdims=True)
+        act = ~done
+        ck[act] ^= flip[act].astype(np.uint8)
+    return ck.astype(np.int8), status, iters
+
+
+def _bp_update(q):
+    """_BP_process (nr_ldpc_decode.py:145-176) on q: (B, d, Zc) float64, every row at once."""
+    B, d, Zc = q.shape
+    t = np.tanh(q / 2)
+    zero = q == 0
+    nz = zero.sum(axis=1)
+    prod = t[:, 0].copy()
+    for k in range(1, d):                     # np.prod: left-to-right
+        prod = prod * t[:, k]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tmp2 = prod[:, None, :] / t
+        r = np.where(tmp2 >= 1, 2 * 19.07, np.where(tmp2 <= -1, -2 * 19.07,
+                                                     2 * np.arctanh(np.clip(tmp2, -1, 1))))
+    r = np.where((nz == 0)[:, None, :], r, 0.0)
+    # one zero: that edge gets prod(t[0:zk]) * prod(t[zk+1:]) (no atanh, as the reference)
+    one = nz == 1
+    if one.any():
+        zk = np.argmax(zero, axis=1)
+        pa = np.ones((B, Zc))
+        pb = np.ones((B, Zc))
+        first_a = np.ones((B, Zc), bool)
+        first_b = np.ones((B, Zc), bool)
+        for k in range(d):
+            ina = k < zk
+            pa = np.where(ina, np.where(first_a, t[:, k], pa * t[:, k]), pa)
+            first_a &= ~ina
+            inb = k > zk
+            pb = np.where(inb, np.where(first_b, t[:, k], pb * t[:, k]), pb)
+            first_b &= ~inb
+        val = pa * pb
+        for k in range(d):
+            r[:, k] = np.where(one & (zk == k), val, r[:, k])
+    return r
+
+
+def decode_bp(llr, Zc, bgn, L, full=False):
+    """nr_decode_ldpc(..., algo='BP'): the flooding loop of decode_ldpc (:51-143) with the
+    sum-product check-node update _BP_process (:145-176), float64, batched."""
+    T = np.float64
+    llr = np.atleast_2d(np.asarray(llr, T))
+    g = graph(bgn, Zc)
+    B = llr.shape[0]
+    Lfull = llr.copy() if full else np.concatenate([np.zeros((B, 2 * Zc), T), llr], axis=1)
+    LQ = Lfull.copy()
+    Lr = [np.zeros((B, g.rs[i + 1] - g.rs[i], Zc), T) for i in range(g.Mb)]
+    done = np.zeros(B, bool)
+    ck = np.zeros((B, g.Nf), np.int8)
+    status = np.zeros(B, bool)
+    iters = np.full(B, L, np.int32)
+    for it in range(L):
+        hd = LQ < 0
+        ok = ~_row_hd_fail(hd, g) & ~done
+        ck[ok] = hd[ok]
+        status[ok] = True
+        iters[ok] = it
+        done |= ok
+        if done.all():
+            break
+        act = ~done
+        acc = np.zeros((B, g.Nf), T)
+        newLr = []
+        for i in range(g.Mb):
+            cols = g.rows_cols(i)
+            r = _bp_update(LQ[:, cols] - Lr[i])
+            newLr.append(r)
+            acc[:, cols] += r
+        LQn = Lfull + acc
+        LQ[act] = LQn[act]
+        for i in range(g.Mb):
+            Lr[i][act] = newLr[i][act]
+    rem = ~done
+    if rem.any():
+        hd = LQ <= 0
+        fail = _row_hd_fail(hd, g)
+        ck[rem] = hd[rem]
+        status[rem] = ~fail[rem]
     return ck, status, iters
 
 

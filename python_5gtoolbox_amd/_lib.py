@@ -28,6 +28,13 @@ SIGNATURES = {
                                           _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
                                           _c.c_double, _c.c_double, _c.c_int32, _c.c_int32,
                                           _c.c_void_p]),
+    "ldpc5g_decode_bf": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                    _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
+                                    _c.c_int64, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_bp_scratch_elems": (_c.c_int64, [_c.c_int32, _c.c_int32, _c.c_int32]),
+    "ldpc5g_decode_bp": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                    _c.c_int64, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
+                                    _c.c_int32, _c.c_int64, _c.c_int64, _c.c_void_p]),
     "ldpc5g_last_error": (_c.c_char_p, []),
     "ldpc5g_version": (_c.c_char_p, []),
 }

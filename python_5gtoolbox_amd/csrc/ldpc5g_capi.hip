@@ -1,0 +1,231 @@
+// ldpc5g_capi.hip — the extern "C" boundary of libldpc5g.so (include/ldpc5g.h): argument
+// validation, error codes, mixed-batch work lists; kernels live in ldpc5g_{enc,dec,bfbp}.hip.
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ldpc5g_common.h"
+
+namespace ldpc5g_impl {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int zc_index(int Zc) {
+    for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
+        if (kLdpcZcList[i] == Zc) return i;
+    return -1;
+}
+
+int check_hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(LDPC5G_EHIP, "%s: %s", what, hipGetErrorString(e));
+    return LDPC5G_OK;
+}
+
+namespace {
+// per-device scratch for the mixed path's work lists
+struct MixedScratch {
+    void* dev = nullptr;
+    size_t cap = 0;
+};
+std::mutex g_mix_mu;
+MixedScratch g_mix[64];
+}  // namespace
+
+}  // namespace ldpc5g_impl
+
+using namespace ldpc5g_impl;
+
+// ================================================================================== C ABI
+extern "C" {
+
+const char* ldpc5g_version(void) { return LDPC5G_VERSION; }
+
+const char* ldpc5g_last_error(void) { return g_err.c_str(); }
+
+int ldpc5g_find_ils(int32_t Zc) {
+    int i = zc_index(Zc);
+    return i < 0 ? 255 : kLdpcZcSet[i];
+}
+
+int ldpc5g_encode(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t Zc, int64_t ldk,
+                  int64_t ldn, void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int K = (bgn == 1 ? 22 : 10) * Zc, N = (bgn == 1 ? 66 : 50) * Zc;
+    if (B < 0 || ldk < K || ldn < N) return fail(LDPC5G_ESIZE, "bad sizes B=%d ldk=%lld ldn=%lld (K=%d N=%d)", B, (long long)ldk, (long long)ldn, K, N);
+    if (B == 0) return LDPC5G_OK;
+    if (!ck || !dn) return fail(LDPC5G_ESIZE, "null buffer");
+    return launch_encode(ck, dn, B, bgn, Zc, zi, ldk, ldn, (hipStream_t)stream);
+}
+
+int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
+                     int32_t* iters, int32_t B, int32_t bgn, int32_t Zc, int32_t L, double alpha,
+                     double beta, int32_t schedule, int32_t flags, int64_t ldl, int64_t ldc,
+                     void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
+    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+        return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
+    if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
+    if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
+    if (schedule == LDPC5G_LAYERED && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "layered schedule requires float32 LLRs");
+    if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
+    if (B == 0) return LDPC5G_OK;
+    if (!llr || !ck || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
+    return launch_dec(bgn, llr_dtype, schedule == LDPC5G_LAYERED, llr, ck, status, iters, B, Zc, zi,
+                      ldl, ldc, L, alpha, beta, pc, (hipStream_t)stream);
+}
+
+int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
+                     int32_t* iters, int32_t B, int32_t bgn, int32_t Zc, int32_t L, int32_t flags,
+                     int64_t ldl, int64_t ldc, void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
+    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+        return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
+    if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
+    if (B == 0) return LDPC5G_OK;
+    if (!llr || !ck || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
+    return launch_bf(bgn, llr_dtype, llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, pc,
+                     (hipStream_t)stream);
+}
+
+int64_t ldpc5g_bp_scratch_elems(int32_t B, int32_t bgn, int32_t Zc) {
+    if ((bgn != 1 && bgn != 2) || B < 0 || zc_index(Zc) < 0) return -1;
+    return (int64_t)B * edges_of_bg(bgn) * Zc;
+}
+
+int ldpc5g_decode_bp(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                     double* scratch, int64_t scratch_elems, int32_t B, int32_t bgn, int32_t Zc,
+                     int32_t L, int32_t flags, int64_t ldl, int64_t ldc, void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
+    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+        return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
+    if (scratch_elems < ldpc5g_bp_scratch_elems(B, bgn, Zc))
+        return fail(LDPC5G_ESIZE, "scratch too small: %lld < %lld", (long long)scratch_elems, (long long)ldpc5g_bp_scratch_elems(B, bgn, Zc));
+    if (B == 0) return LDPC5G_OK;
+    if (!llr || !ck || !status || !iters || !scratch) return fail(LDPC5G_ESIZE, "null buffer");
+    return launch_bp(bgn, llr, ck, status, iters, scratch, B, Zc, zi, ldl, ldc, L, pc,
+                     (hipStream_t)stream);
+}
+
+int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* llr_base,
+                           int32_t llr_dtype, int8_t* ck_base, uint8_t* status, int32_t* iters,
+                           int32_t L, double alpha, double beta, int32_t schedule, int32_t flags,
+                           void* stream) {
+    g_err.clear();
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    if (B < 0 || L < 0) return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d", B, L);
+    if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
+    if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
+    if (schedule == LDPC5G_LAYERED && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "layered schedule requires float32 LLRs");
+    if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
+    if (B == 0) return LDPC5G_OK;
+    if (!desc || !llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
+    // group codeblocks by (bgn, Zc), pack G = floor(384/Zc) per workgroup
+    std::vector<std::vector<int>> bucket[2];
+    bucket[0].resize(LDPC5G_NUM_ZC);
+    bucket[1].resize(LDPC5G_NUM_ZC);
+    for (int b = 0; b < B; ++b) {
+        const ldpc5g_cb_desc_t& d = desc[b];
+        if (d.bgn != 1 && d.bgn != 2) return fail(LDPC5G_EBGN, "desc[%d]: bgn must be 1 or 2 (got %d)", b, d.bgn);
+        int zi = zc_index(d.Zc);
+        if (zi < 0) return fail(LDPC5G_EZC, "desc[%d]: Zc=%d is not a lifting size", b, d.Zc);
+        if (d.llr_off < 0 || d.ck_off < 0) return fail(LDPC5G_ESIZE, "desc[%d]: negative offset", b);
+        bucket[d.bgn - 1][zi].push_back(b);
+    }
+    std::vector<DecWork> work[2];
+    std::vector<CbRef> refs;
+    for (int g = 0; g < 2; ++g)
+        for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
+            const std::vector<int>& v = bucket[g][zi];
+            const int Zc = kLdpcZcList[zi], G = dec_G(Zc);
+            for (size_t s = 0; s < v.size(); s += G) {
+                DecWork w;
+                w.zi = zi, w.Zc = Zc, w.G = (int)std::min<size_t>(G, v.size() - s), w.first = (int)refs.size();
+                for (int c = 0; c < w.G; ++c) {
+                    CbRef r;
+                    r.llr_off = desc[v[s + c]].llr_off, r.ck_off = desc[v[s + c]].ck_off, r.out = v[s + c], r.pad = 0;
+                    refs.push_back(r);
+                }
+                work[g].push_back(w);
+            }
+        }
+    const size_t wbytes = (work[0].size() + work[1].size()) * sizeof(DecWork);
+    const size_t rbytes = refs.size() * sizeof(CbRef);
+    const size_t need = wbytes + rbytes;
+    int dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<unsigned char> host(need);
+    memcpy(host.data(), work[0].data(), work[0].size() * sizeof(DecWork));
+    memcpy(host.data() + work[0].size() * sizeof(DecWork), work[1].data(), work[1].size() * sizeof(DecWork));
+    memcpy(host.data() + wbytes, refs.data(), rbytes);
+    unsigned char* dbuf;
+    {
+        std::lock_guard<std::mutex> lk(g_mix_mu);
+        MixedScratch& s = g_mix[dev & 63];
+        if (s.cap < need) {
+            if (s.dev) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(s.dev);
+            }
+            s.dev = nullptr;
+            s.cap = 0;
+            if (int rc = check_hip(hipMalloc(&s.dev, need * 2), "hipMalloc(work list)")) return rc;
+            s.cap = need * 2;
+        }
+        dbuf = (unsigned char*)s.dev;
+        // the work list is consumed by this call's kernels; a later call on another stream
+        // would overwrite it, so the copy + launches are serialised on this stream and the
+        // host waits for the copy before returning the buffer to the pool
+        if (int rc = check_hip(hipMemcpyAsync(dbuf, host.data(), need, hipMemcpyHostToDevice, st), "hipMemcpyAsync(work list)")) return rc;
+        const DecWork* w1 = (const DecWork*)dbuf;
+        const DecWork* w2 = w1 + work[0].size();
+        const CbRef* r = (const CbRef*)(dbuf + wbytes);
+        const bool lay = schedule == LDPC5G_LAYERED;
+        for (int g = 0; g < 2; ++g) {
+            const int nwg = (int)work[g].size();
+            if (!nwg) continue;
+            const DecWork* w = g == 0 ? w1 : w2;
+            int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg, w, r,
+                                      L, alpha, beta, pc, st);
+            if (rc) return rc;
+        }
+        if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize(mixed)")) return rc;
+    }
+    return LDPC5G_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,111 @@
+// ldpc5g_common.h — shared device/host definitions of the MI355X 5G NR LDPC engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "ldpc5g_tables.h"
+#include "ldpc5g.h"
+
+#define LDPC5G_VERSION "ldpc5g 0.2.0 gfx950"
+
+namespace ldpc5g_impl {
+
+// ------------------------------------------------------------------------------ base graphs
+template <int BG>
+struct BGT;
+template <>
+struct BGT<1> {
+    static constexpr int MB = LDPC5G_BG1_ROWS;   // 46 base rows
+    static constexpr int NB = LDPC5G_BG1_COLS;   // 68 base columns
+    static constexpr int KB = 22;                // information columns
+    static constexpr int KC = 26;                // core columns (degree > 1): info + 4 parity
+    static constexpr int E = LDPC5G_BG1_EDGES;   // 316
+    static constexpr const int16_t* RS = kBG1RowStart;
+    static constexpr const int8_t* COL = kBG1Col;
+};
+template <>
+struct BGT<2> {
+    static constexpr int MB = LDPC5G_BG2_ROWS;   // 42
+    static constexpr int NB = LDPC5G_BG2_COLS;   // 52
+    static constexpr int KB = 10;
+    static constexpr int KC = 14;
+    static constexpr int E = LDPC5G_BG2_EDGES;   // 197
+    static constexpr const int16_t* RS = kBG2RowStart;
+    static constexpr const int8_t* COL = kBG2Col;
+};
+
+template <int BG>
+constexpr int edge_of(int i, int j) {
+    for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i + 1]; ++e)
+        if (BGT<BG>::COL[e] == j) return e;
+    return -1;
+}
+
+// V(i,j) mod Zc of edge e for lifting size index zi (tables packed 2 edges per 32-bit word so a
+// wave-uniform read is a scalar load)
+template <int BG>
+__device__ __forceinline__ int shift_of(int zi, int e) {
+    uint32_t w;
+    if constexpr (BG == 1) w = kBG1ShiftMod[zi][e >> 1];
+    else w = kBG2ShiftMod[zi][e >> 1];
+    return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+}
+template <int BG>
+__device__ __forceinline__ int row_start_d(int i) {
+    if constexpr (BG == 1) return kBG1RowStartD[i];
+    else return kBG2RowStartD[i];
+}
+template <int BG>
+__device__ __forceinline__ int col_d(int e) {
+    if constexpr (BG == 1) return kBG1ColD[e];
+    else return kBG2ColD[e];
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int I, int E, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        sfor<I + 1, E>(f);
+    }
+}
+
+
+struct DecWork {     // one workgroup of the mixed-Zc path
+    int32_t zi, Zc, G, first;
+};
+struct CbRef {       // one codeblock of the mixed-Zc path
+    int64_t llr_off, ck_off;
+    int32_t out, pad;
+};
+
+constexpr int kDecThreads = 384;   // = max Zc: one thread per check row z of a base row
+constexpr int kCS = kDecThreads;   // LDS column stride (entries): G*Zc <= 384 always
+
+inline int dec_G(int Zc) { return Zc >= kDecThreads ? 1 : kDecThreads / Zc; }
+
+// ---- host helpers (ldpc5g_capi.hip)
+int fail(int code, const char* fmt, ...);
+int zc_index(int Zc);
+int check_hip(hipError_t e, const char* what);
+
+// ---- launchers (one per translation unit)
+int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,
+                  int64_t ldn, hipStream_t st);
+int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
+               int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
+               double alpha, double beta, int pc, hipStream_t st);
+int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
+                     uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
+                     const CbRef* cbs, int L, double alpha, double beta, int pc, hipStream_t st);
+int launch_bf(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+              int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc, hipStream_t st);
+int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+              double* msg, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc,
+              hipStream_t st);
+int edges_of_bg(int bgn);
+
+}  // namespace ldpc5g_impl

@@ -1,0 +1,468 @@
+// ldpc5g_dec.hip — flooding / layered min-sum decoder (py5gphy/ldpc/nr_ldpc_decode.py:11-143, 178-227)
+// Part of libldpc5g.so (MI355X, gfx950); reference mapping in ldpc5g_common.h / DESIGN.md §4.
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "ldpc5g_common.h"
+
+namespace ldpc5g_impl {
+namespace {
+// ================================================================================== DECODER
+template <typename T>
+struct FT;
+template <>
+struct FT<float> {
+    __device__ static __forceinline__ uint32_t sbits(float x) { return __float_as_uint(x); }
+    // x with its sign bit XORed by bit 31 of `b`
+    __device__ static __forceinline__ float xsign(float x, uint32_t b) {
+        return __uint_as_float(__float_as_uint(x) ^ (b & 0x80000000u));
+    }
+    __device__ static __forceinline__ float inf() { return __uint_as_float(0x7f800000u); }
+    __device__ static __forceinline__ float med3(float a, float b, float c) {
+        return __builtin_amdgcn_fmed3f(a, b, c);
+    }
+};
+template <>
+struct FT<double> {
+    __device__ static __forceinline__ uint32_t sbits(double x) { return (uint32_t)__double2hiint(x); }
+    __device__ static __forceinline__ double xsign(double x, uint32_t b) {
+        return __longlong_as_double(__double_as_longlong(x) ^ ((long long)(b & 0x80000000u) << 32));
+    }
+    __device__ static __forceinline__ double inf() { return __longlong_as_double(0x7ff0000000000000ll); }
+    __device__ static __forceinline__ double med3(double a, double b, double c) {
+        return fmax(fmin(a, b), fmin(fmax(a, b), c));
+    }
+};
+
+// Compressed check-node state of one row: r_k = (k == idx ? mB : mA), sign = bit k of pk.
+// pk: bits 0..deg-1 = sign of r_k, bits 24..28 = idx (an edge holding min |q|).
+template <typename T>
+__device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, uint32_t idx, int k) {
+    return FT<T>::xsign((idx == (uint32_t)k) ? mB : mA, pk << (31 - k));
+}
+
+// Consecutive base rows with disjoint core columns form one barrier group: processing them
+// together is identical to processing them one after another (layered) and keeps the
+// row-ascending accumulation order of every column (flooding).  BG1: 46 rows -> 32 groups,
+// BG2: 42 -> 28.
+template <int BG>
+struct RowGroups {
+    int n = 0;
+    int start[64] = {};
+    constexpr RowGroups() {
+        using P = BGT<BG>;
+        int g0 = 0;
+        start[0] = 0;
+        n = 1;
+        for (int i = 1; i < P::MB; ++i) {
+            bool dis = true;
+            for (int a = g0; a < i && dis; ++a)
+                for (int e = P::RS[a]; e < P::RS[a + 1]; ++e)
+                    for (int f = P::RS[i]; f < P::RS[i + 1]; ++f)
+                        if (P::COL[e] == P::COL[f] && P::COL[e] < P::KC) dis = false;
+            if (!dis) {
+                start[n++] = i;
+                g0 = i;
+            }
+        }
+        start[n] = P::MB;
+    }
+};
+template <int BG>
+constexpr RowGroups<BG> kGroups{};
+
+// Packed shift words (2 edges per word) spanned by the edges of row group g.
+template <int BG>
+constexpr int group_w0(int g) { return BGT<BG>::RS[kGroups<BG>.start[g]] >> 1; }
+template <int BG>
+constexpr int group_nw(int g) {
+    return ((BGT<BG>::RS[kGroups<BG>.start[g + 1]] - 1) >> 1) - group_w0<BG>(g) + 1;
+}
+template <int BG>
+constexpr int max_group_nw() {
+    int m = 0;
+    for (int g = 0; g < kGroups<BG>.n; ++g) m = m > group_nw<BG>(g) ? m : group_nw<BG>(g);
+    return m;
+}
+template <int BG>
+__device__ __forceinline__ uint32_t shift_word(int zi, int w) {
+    if constexpr (BG == 1) return kBG1ShiftMod[zi][w];
+    else return kBG2ShiftMod[zi][w];
+}
+
+
+template <typename T, bool LAYERED>
+constexpr size_t dec_lds_bytes_t(int MB, int KC) {
+    return (size_t)KC * kCS * sizeof(T) * (LAYERED ? 1 : 2) +
+           (sizeof(T) == 4 ? (size_t)(MB - 4) * kCS * sizeof(T) : 0) + 2 * kCS * sizeof(int);
+}
+
+template <int BG, typename T, bool LAYERED>
+__global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
+    const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
+    int L, T alpha, T beta, int pc, const DecWork* __restrict__ work,
+    const CbRef* __restrict__ cbs) {
+    // pc = number of leading punctured block columns absent from the LLR rows (2, or 0 when the
+    // caller passes full-length rows as decode_ldpc(LLRin, H, ...) does, nr_ldpc_decode.py:51)
+    using P = BGT<BG>;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
+    constexpr bool XL_LDS = TS == 4;
+    constexpr int ACC_B = KC * kCS * TS;                        // byte offsets in LDS
+    constexpr int XL_B = KC * kCS * TS * (LAYERED ? 1 : 2);
+    constexpr int FLAG_B = XL_B + (XL_LDS ? (MB - 4) * kCS * TS : 0);
+    extern __shared__ __align__(16) unsigned char smem[];
+
+    int Zc = Zc_u, zi = zi_u, G = G_u;
+    const int t = threadIdx.x;
+    if (work) {
+        DecWork w = work[blockIdx.x];
+        Zc = w.Zc, zi = w.zi, G = w.G;
+    }
+    const int cbl = t / Zc;
+    const int z = t - cbl * Zc;
+    bool valid = cbl < G;
+    const T* lrow = llr;
+    int8_t* crow = ck;
+    int out = 0;
+    if (valid) {
+        if (work) {
+            CbRef r = cbs[work[blockIdx.x].first + cbl];
+            lrow = llr + r.llr_off;
+            crow = ck + r.ck_off;
+            out = r.out;
+        } else {
+            int cb = blockIdx.x * G + cbl;
+            valid = cb < B;
+            lrow = llr + (int64_t)cb * ldl;
+            crow = ck + (int64_t)cb * ldc;
+            out = cb;
+        }
+    }
+    const int cl = valid ? cbl : 0;
+    const int tzb = (cl * Zc + z) * TS;   // byte offset of this thread's own column entry
+    const int ZcT = Zc * TS;
+    int zv = z, ziv = zi;   // made opaque per iteration (see the iteration loop)
+    int* flagA = (int*)(smem + FLAG_B);
+    int* flagB = flagA + kCS;
+    auto at = [&](int byte) -> T& { return *(T*)(smem + byte); };
+    auto own = [&](int j) -> T& { return at(j * kCS * TS + tzb); };
+    // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
+    auto llrx = [&](int i4) -> T {
+        if constexpr (XL_LDS) return at(XL_B + i4 * kCS * TS + tzb);
+        else return lrow[(KB + 4 + i4 - pc) * Zc + zv];
+    };
+
+    // per-thread state of rows (i, z), i = 0..MB-1
+    T sA[MB], sB[MB];
+    uint32_t sP[MB];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) sA[i] = T(0), sB[i] = T(0), sP[i] = 0u;
+
+    uint32_t hdc_prev = 0;   // layered: hard decisions of own core columns, last iteration end
+    uint64_t hdx_prev = 0;   // layered: ... of own extension columns
+    if (valid) {
+        for (int j = 0; j < KC; ++j) {
+            const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
+            own(j) = v;
+            if (!LAYERED) at(ACC_B + j * kCS * TS + tzb) = T(0);
+            hdc_prev |= (uint32_t)(v < T(0)) << j;
+        }
+        for (int i4 = 0; i4 < MB - 4; ++i4) {
+            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            if constexpr (XL_LDS) at(XL_B + i4 * kCS * TS + tzb) = v;
+            hdx_prev |= (uint64_t)(v < T(0)) << i4;
+        }
+    }
+    if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+    bool active = valid;
+    __syncthreads();
+
+    // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
+    auto rot = [&](int s) -> int { return tzb + s * TS - (zv >= Zc - s ? ZcT : 0); };
+
+    int it = 0;
+    for (; it < L; ++it) {
+        // zv / ziv are re-materialised opaque each iteration: otherwise LICM hoists the ~300
+        // loop-invariant column addresses (z + V) mod Zc out of the loop into VGPRs/SGPRs.
+        zv = z;
+        ziv = zi;
+        asm volatile("" : "+v"(zv));
+        asm volatile("" : "+s"(ziv));
+        bool fail = false;
+        uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
+        // the next row group's packed shift words are loaded (scalar, wave-uniform) before the
+        // barrier that precedes the group, so their latency hides behind it
+        constexpr int NPW = max_group_nw<BG>();
+        uint32_t nsw[NPW];
+        auto prefetch = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            sfor<0, group_nw<BG>(g)>([&](auto wc) {
+                constexpr int w = decltype(wc)::value;
+                nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
+            });
+        };
+        prefetch(std::integral_constant<int, 0>{});
+        sfor<0, kGroups<BG>.n>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
+            auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
+                return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+            };
+            if (active) {
+                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    constexpr int e0 = P::RS[i];
+                    constexpr int d = P::RS[i + 1] - e0;
+                    const T mA = sA[i], mB = sB[i];
+                    const uint32_t pk = sP[i];
+                    const uint32_t idxo = pk >> 24;
+                    T q[d];
+                    int rb[d];
+                    T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+                    uint32_t sx = 0, idx = 0, negs = 0;
+                    bool par = false;
+                    // ---- pass 1: variable-to-check messages q, two-min, sign product
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        const T rold = decomp(mA, mB, pk, idxo, k);
+                        T qq;
+                        if constexpr (j < KC) {
+                            rb[k] = rot(gshift(e0 + k));
+                            const T a = at(j * kCS * TS + rb[k]);
+                            qq = a - rold;
+                            if constexpr (!LAYERED) par ^= a < T(0);
+                        } else if constexpr (LAYERED) {
+                            qq = llrx(i - 4);   // degree-1 column: q is the channel LLR itself
+                        } else {
+                            const T a = llrx(i - 4) + rold;   // LQ of a degree-1 column
+                            qq = a - rold;
+                            const bool h = a < T(0);
+                            par ^= h;
+                            hdx |= (uint64_t)h << (i - 4);
+                        }
+                        q[k] = qq;
+                        const T aq = fabs(qq);
+                        if constexpr (!LAYERED) {
+                            idx = aq < min1 ? (uint32_t)k : idx;
+                            negs |= (FT<T>::sbits(qq) >> 31) << k;
+                        }
+                        min2 = FT<T>::med3(min1, min2, aq);
+                        min1 = fmin(min1, aq);
+                        sx ^= FT<T>::sbits(qq);
+                    });
+                    fail |= par;
+                    const T x1 = min1 - beta, x2 = min2 - beta;
+                    const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
+                    const T nB = alpha * (x2 > T(0) ? x2 : T(0));
+                    // ---- pass 2: check-to-variable messages r = sign * (k == argmin ? nB : nA)
+                    uint32_t signs = 0, idxn = 0;
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        T r;
+                        if constexpr (LAYERED) {
+                            const T aq = fabs(q[k]);
+                            const bool isMin = aq == min1;   // ties: nB == nA, either is right
+                            idxn = isMin ? (uint32_t)k : idxn;
+                            const uint32_t sb = FT<T>::sbits(q[k]) ^ sx;
+                            r = FT<T>::xsign(isMin ? nB : nA, sb);
+                            signs |= (sb >> 31) << k;
+                            if constexpr (j < KC) {
+                                at(j * kCS * TS + rb[k]) = q[k] + r;
+                            } else {
+                                hdx |= (uint64_t)(llrx(i - 4) + r < T(0)) << (i - 4);
+                            }
+                        } else {
+                            const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
+                            r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
+                            if constexpr (j < KC) {
+                                T& a = at(ACC_B + j * kCS * TS + rb[k]);
+                                a = a + r;   // row-ascending accumulation (:126)
+                            }
+                        }
+                    });
+                    sA[i] = nA;
+                    sB[i] = nB;
+                    if constexpr (LAYERED) sP[i] = signs | (idxn << 24);
+                    else sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
+                });
+            }
+            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
+            __syncthreads();
+        });
+
+        if constexpr (!LAYERED) {
+            // ---- reference order: the syndrome of LQ at the start of the pass decides (:107-114)
+            if (active && fail) flagA[cl] = 1;
+            __syncthreads();
+            const bool conv = active && flagA[cl] == 0;
+            if (conv) {
+                for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
+                for (int i4 = 0; i4 < MB - 4; ++i4)
+                    crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
+                if (z == 0) status[out] = 1, iters[out] = it;
+                active = false;
+            } else if (active) {
+                for (int j = 0; j < KC; ++j) {
+                    T& acc = at(ACC_B + j * kCS * TS + tzb);
+                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
+                    own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
+                    acc = T(0);
+                }
+            }
+        } else {
+            // ---- layered stopping rule: no hard decision changed over the iteration, then an
+            //      exact syndrome check of those decisions (oracle.decode_layered)
+            uint32_t hdc = 0;
+            if (active)
+                for (int j = 0; j < KC; ++j) hdc |= (uint32_t)(own(j) < T(0)) << j;
+            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;
+            hdc_prev = hdc;
+            hdx_prev = hdx;
+            __syncthreads();
+            const bool cand = active && flagA[cl] == 0;
+            if (__syncthreads_or(cand)) {
+                if (cand) {
+                    bool sf = false;
+                    sfor<0, MB>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        constexpr int e0 = P::RS[i];
+                        constexpr int d = P::RS[i + 1] - e0;
+                        bool par = false;
+                        sfor<0, d>([&](auto kc) {
+                            constexpr int k = decltype(kc)::value;
+                            constexpr int j = P::COL[e0 + k];
+                            if constexpr (j < KC)
+                                par ^= at(j * kCS * TS + rot(shift_of<BG>(ziv, e0 + k))) < T(0);
+                            else
+                                par ^= (bool)((hdx >> (i - 4)) & 1u);
+                        });
+                        sf |= par;
+                    });
+                    if (sf) flagB[cl] = 1;
+                }
+                __syncthreads();
+                if (cand && flagB[cl] == 0) {
+                    for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)((hdc >> j) & 1u);
+                    for (int i4 = 0; i4 < MB - 4; ++i4)
+                        crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
+                    if (z == 0) status[out] = 1, iters[out] = it + 1;
+                    active = false;
+                }
+            }
+        }
+        __syncthreads();
+        if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+        if (!__syncthreads_or(active)) break;
+    }
+
+    // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
+    zv = z;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    if (active) {
+        bool fail = false;
+        sfor<0, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                T a;
+                if constexpr (j < KC) a = at(j * kCS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                else a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
+                par ^= (a <= T(0));
+            });
+            fail |= par;
+        });
+        if (fail) flagA[cl] = 1;
+    }
+    __syncthreads();
+    if (active) {
+        for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+        sfor<4, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+            const T a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, dl);
+            crow[(KB + i) * Zc + zv] = (int8_t)(a <= T(0));
+        });
+        if (z == 0) {
+            status[out] = flagA[cl] == 0;
+            iters[out] = L;
+        }
+    }
+}
+
+template <int BG, typename T, bool LAYERED>
+size_t dec_lds_bytes() {
+    return dec_lds_bytes_t<T, LAYERED>(BGT<BG>::MB, BGT<BG>::KC);
+}
+
+template <int BG, typename T, bool LAYERED>
+int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                 int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    auto kern = ldpc_dec_kernel<BG, T, LAYERED>;
+    const int G = dec_G(Zc);
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
+    const int threads = ((G * Zc + 63) / 64) * 64;
+    const int grid = (B + G - 1) / G;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, llr, ck, status, iters, B, Zc, zi,
+                       G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
+                       (const CbRef*)nullptr);
+    return check_hip(hipGetLastError(), "ldpc_dec_kernel launch");
+}
+
+template <int BG, typename T, bool LAYERED>
+int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                       const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
+                       int pc, hipStream_t st) {
+    auto kern = ldpc_dec_kernel<BG, T, LAYERED>;
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kDecThreads), lds, st, llr, ck, status, iters, 0, 0,
+                       0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
+    return check_hip(hipGetLastError(), "ldpc_dec_kernel(mixed) launch");
+}
+
+}  // namespace
+
+int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
+               int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
+               double alpha, double beta, int pc, hipStream_t st) {
+    if (dtype == LDPC5G_F64) {
+        const double* p = (const double*)llr;
+        return bgn == 1 ? launch_dec_t<1, double, false>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                        : launch_dec_t<2, double, false>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    }
+    const float* p = (const float*)llr;
+    if (bgn == 1)
+        return layered ? launch_dec_t<1, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                       : launch_dec_t<1, float, false>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    return layered ? launch_dec_t<2, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                   : launch_dec_t<2, float, false>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+}
+
+int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
+                     uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
+                     const CbRef* cbs, int L, double alpha, double beta, int pc, hipStream_t st) {
+    if (dtype == LDPC5G_F64) {
+        const double* p = (const double*)llr;
+        return bgn == 1 ? launch_dec_mixed_t<1, double, false>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                        : launch_dec_mixed_t<2, double, false>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    }
+    const float* p = (const float*)llr;
+    if (bgn == 1)
+        return layered ? launch_dec_mixed_t<1, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                       : launch_dec_mixed_t<1, float, false>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    return layered ? launch_dec_mixed_t<2, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                   : launch_dec_mixed_t<2, float, false>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+}
+
+}  // namespace ldpc5g_impl

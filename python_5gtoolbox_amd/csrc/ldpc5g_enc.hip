@@ -1,0 +1,459 @@
+// ldpc5g_enc.hip — QC-LDPC encoder kernels (py5gphy/ldpc/nr_ldpc_encode.py:8-115)
+// Part of libldpc5g.so (MI355X, gfx950); reference mapping in ldpc5g_common.h / DESIGN.md §4.
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "ldpc5g_common.h"
+
+namespace ldpc5g_impl {
+namespace {
+// ================================================================================== ENCODER
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+}
+
+// 32 bits starting at bit `bit` of a packed LSB-first vector (needs one word of padding).
+__device__ __forceinline__ uint32_t window32(const uint32_t* v, int bit) {
+    return funnel(v[(bit >> 5) + 1], v[bit >> 5], (uint32_t)bit);
+}
+
+// bit b of the result = block[(start + b) mod Zc], where block is the Zc-bit vector at bit
+// offset `base` of v.  (P_s x)[m] = x[(m+s) mod Zc] is one shifted identity block of H
+// (ldpc_info.py:124-137), so this is a 32-row slice of a block product.
+__device__ uint32_t fetch_rot32(const uint32_t* v, int base, int Zc, int start) {
+    uint32_t out = 0;
+    int b = 0, pos = start;
+    while (b < 32) {
+        int n = min(32 - b, Zc - pos);
+        uint32_t w = window32(v, base + pos);
+        if (n < 32) w &= (1u << n) - 1u;
+        out |= w << b;
+        b += n;
+        pos += n;
+        if (pos >= Zc) pos = 0;
+    }
+    return out;
+}
+
+__device__ __forceinline__ int mod_zc(int x, int Zc) {   // x in [0, 3*Zc + 64)
+    while (x >= Zc) x -= Zc;
+    return x;
+}
+
+// OR the low n (<=32) bits of val into the packed vector at bit offset `bit`.
+__device__ __forceinline__ void or_bits(uint32_t* v, int bit, uint32_t val, int n) {
+    if (n < 32) val &= (1u << n) - 1u;
+    if (!val) return;
+    int w = bit >> 5, s = bit & 31;
+    atomicOr(&v[w], val << s);
+    if (s) {
+        uint32_t hi = val >> (32 - s);
+        if (hi) atomicOr(&v[w + 1], hi);
+    }
+}
+
+struct EncLayout {
+    int K, N, W, DW, KW, PBW, words;
+};
+template <int BG>
+__host__ __device__ inline EncLayout enc_layout(int Zc) {
+    using P = BGT<BG>;
+    EncLayout L;
+    L.K = P::KB * Zc;
+    L.N = (P::NB - 2) * Zc;
+    L.W = (Zc + 31) >> 5;
+    L.DW = 2 * L.W + 2;
+    L.KW = (L.K + 31) >> 5;
+    L.PBW = ((P::MB * Zc + 31) >> 5) + 2;
+    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W] | PB[PBW] | raw bytes (K, rounded to 16)
+    L.words = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + L.PBW;
+    L.words = (L.words + 3) & ~3;
+    return L;
+}
+template <int BG>
+inline size_t enc_lds_bytes(int Zc) {
+    EncLayout L = enc_layout<BG>(Zc);
+    return (size_t)L.words * 4 + (((size_t)L.K + 15) & ~(size_t)15);
+}
+
+__device__ __forceinline__ uint32_t expand4(uint32_t b4) {   // 4 bits -> 4 bytes of 0/1
+    return (b4 * 0x00204081u) & 0x01010101u;
+}
+
+template <int BG>
+__global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict__ ck,
+                                                       int8_t* __restrict__ dn, int B, int Zc,
+                                                       int zi, int64_t ldk, int64_t ldn) {
+    using P = BGT<BG>;
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int t = threadIdx.x;
+    const int NT = blockDim.x;
+    const EncLayout Ly = enc_layout<BG>(Zc);
+    const int K = Ly.K, N = Ly.N, W = Ly.W, DW = Ly.DW, KW = Ly.KW;
+    const int S = K - 2 * Zc;   // systematic bytes in dn
+    extern __shared__ __align__(16) uint32_t sm[];
+    uint32_t* ib = sm;
+    uint32_t* X = ib + KW + 2;
+    uint32_t* lam = X + P::KC * DW;
+    uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
+    uint32_t* PB = pv + 5 * W;
+    int8_t* raw = (int8_t*)(sm + Ly.words);
+    // ---- 1. load info bytes, keep them raw in LDS, pack parity bits (fillers -> 0)
+    const int8_t* src = ck + (int64_t)b * ldk;
+    const bool al16 = (((uintptr_t)src) & 15) == 0;
+    const int twoZ = 2 * Zc;
+    for (int wi = t; wi < KW; wi += NT) {
+        const int base = wi * 32;
+        uint32_t bits = 0;
+        if (al16 && base + 32 <= K) {
+            int4 v[2];
+            v[0] = *(const int4*)(src + base);
+            v[1] = *(const int4*)(src + base + 16);
+            *(int4*)(raw + base) = v[0];
+            *(int4*)(raw + base + 16) = v[1];
+            const uint32_t* d = (const uint32_t*)v;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    uint32_t by = (d[q] >> (8 * y)) & 0xffu;
+                    int pos = base + 4 * q + y;
+                    uint32_t bit = (by & 1u) & ~((uint32_t)(pos >= twoZ && by == 0xffu));
+                    bits |= bit << (4 * q + y);
+                }
+            }
+        } else {
+            for (int y = 0; y < 32; ++y) {
+                int pos = base + y;
+                if (pos < K) {
+                    uint32_t by = (uint8_t)src[pos];
+                    raw[pos] = (int8_t)by;
+                    uint32_t bit = (by & 1u) & ~((uint32_t)(pos >= twoZ && by == 0xffu));
+                    bits |= bit << y;
+                }
+            }
+        }
+        ib[wi] = bits;
+    }
+    if (t < 2) ib[KW + t] = 0;
+    for (int w = t; w < Ly.PBW; w += NT) PB[w] = 0;
+    __syncthreads();
+
+    // ---- 2. periodic extensions X_j[t] = block_j[t mod Zc] of the information columns
+    for (int task = t; task < P::KB * DW; task += NT) {
+        int j = task / DW, q = task - j * DW;
+        X[j * DW + q] = fetch_rot32(ib, j * Zc, Zc, mod_zc(32 * q, Zc));
+    }
+    __syncthreads();
+
+    // ---- 3. lambda_i = A_i c for the 4 core rows (nr_ldpc_encode.py:92-94)
+    for (int task = t; task < 4 * W; task += NT) {
+        int i = task / W, w = task - i * W;
+        uint32_t acc = 0;
+        for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+            int j = col_d<BG>(e);
+            if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+        }
+        lam[i * W + w] = acc;
+    }
+    __syncthreads();
+
+    // ---- 4. core parity by the double-diagonal recursion (BG1 :95-100, BG2 :101-106)
+    constexpr int eS = (BG == 1) ? edge_of<BG>(1, 22) : edge_of<BG>(2, 10);
+    constexpr int eA = edge_of<BG>(0, P::KB);
+    constexpr int eC = edge_of<BG>(3, P::KB);
+    constexpr int eD = (BG == 1) ? edge_of<BG>(2, 25) : edge_of<BG>(1, 11);
+    static_assert(eS >= 0 && eA >= 0 && eC >= 0 && eD >= 0, "base graph core structure");
+    uint32_t* p1 = pv;
+    uint32_t* p2 = pv + W;
+    uint32_t* p3 = pv + 2 * W;
+    uint32_t* p4 = pv + 3 * W;
+    uint32_t* L2 = pv + 4 * W;
+    for (int w = t; w < W; w += NT) L2[w] = lam[w] ^ lam[W + w] ^ lam[2 * W + w] ^ lam[3 * W + w];
+    // (window reads one word past a vector; those bits are masked, the word exists in LDS)
+    __syncthreads();
+    {
+        const int s1 = shift_of<BG>(zi, eS);
+        // p1 = roll(L2, s1): p1[z] = L2[(z - s1) mod Zc]
+        for (int w = t; w < W; w += NT) p1[w] = fetch_rot32(L2, 0, Zc, mod_zc(mod_zc(32 * w, Zc) + Zc - s1, Zc));
+    }
+    __syncthreads();
+    for (int w = t; w < W; w += NT) {
+        p2[w] = lam[w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eA), Zc));
+        p4[w] = lam[3 * W + w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eC), Zc));
+    }
+    __syncthreads();
+    for (int w = t; w < W; w += NT) {
+        if constexpr (BG == 1) p3[w] = lam[2 * W + w] ^ fetch_rot32(p4, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+        else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+    }
+    __syncthreads();
+
+    // ---- 5. extensions of the 4 core parity columns; core parity bits into PB
+    for (int task = t; task < 4 * DW; task += NT) {
+        int k = task / DW, q = task - k * DW;
+        X[(P::KB + k) * DW + q] = fetch_rot32(pv + k * W, 0, Zc, mod_zc(32 * q, Zc));
+    }
+    for (int task = t; task < 4 * W; task += NT) {
+        int k = task / W, w = task - k * W;
+        or_bits(PB, k * Zc + 32 * w, pv[k * W + w], min(32, Zc - 32 * w));
+    }
+    __syncthreads();
+
+    // ---- 6. extension parity rows 4..MB-1: pe = C [c; p] (nr_ldpc_encode.py:111-112)
+    for (int task = t; task < (P::MB - 4) * W; task += NT) {
+        int i = 4 + task / W, w = task % W;
+        uint32_t acc = 0;
+        for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+            int j = col_d<BG>(e);
+            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+        }
+        or_bits(PB, i * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+    }
+    __syncthreads();
+
+    // ---- 7. dn = [ck[2Zc:K], parity bits] as int8 (16 bytes per lane when aligned)
+    int8_t* dst = dn + (int64_t)b * ldn;
+    const bool dal16 = (((uintptr_t)dst) & 15) == 0;
+    const bool raw4 = (twoZ & 3) == 0;
+    const int nch = (N + 15) >> 4;
+    for (int c = t; c < nch; c += NT) {
+        const int q0 = c * 16;
+        if (dal16 && q0 + 16 <= N) {
+            uint32_t o[4];
+            if (q0 >= S) {   // all parity
+                uint32_t bits = window32(PB, q0 - S);
+#pragma unroll
+                for (int y = 0; y < 4; ++y) o[y] = expand4((bits >> (4 * y)) & 15u);
+            } else if (q0 + 16 <= S && raw4) {   // all systematic
+                const uint32_t* r = (const uint32_t*)(raw + twoZ + q0);
+#pragma unroll
+                for (int y = 0; y < 4; ++y) o[y] = r[y];
+            } else {
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        int q = q0 + 4 * y + x;
+                        uint32_t by = q < S ? (uint8_t)raw[twoZ + q] : ((PB[(q - S) >> 5] >> ((q - S) & 31)) & 1u);
+                        v |= by << (8 * x);
+                    }
+                    o[y] = v;
+                }
+            }
+            *(uint4*)(dst + q0) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (int q = q0; q < min(q0 + 16, N); ++q) {
+                dst[q] = q < S ? raw[twoZ + q] : (int8_t)((PB[(q - S) >> 5] >> ((q - S) & 31)) & 1u);
+            }
+        }
+    }
+}
+
+// Fast encoder: Zc % 16 == 0 and 16-B aligned rows (every BG1/BG2 Zc >= 16 that is a multiple
+// of 16, including the Zc=384 hot path).  Same arithmetic as ldpc_enc_kernel; the differences are
+// where bytes go: systematic bytes are stored straight from the load registers, every parity
+// row-word (32 bits of one base row) is expanded and stored straight to dn as 32 (or 16) bytes,
+// and the p1..p4 recursion runs inside wave 0 with wave-level syncs (no parity bit array, no LDS
+// atomics, 4 workgroup barriers instead of 9).
+struct EncFastLayout {
+    int K, N, W, DW, KW, words;
+};
+template <int BG>
+__host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
+    using P = BGT<BG>;
+    EncFastLayout L;
+    L.K = P::KB * Zc;
+    L.N = (P::NB - 2) * Zc;
+    L.W = (Zc + 31) >> 5;
+    L.DW = 2 * L.W + 2;
+    L.KW = (L.K + 31) >> 5;
+    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2]
+    L.words = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + 2;
+    return L;
+}
+template <int BG>
+inline size_t enc_fast_lds_bytes(int Zc) {
+    return (size_t)enc_fast_layout<BG>(Zc).words * 4;
+}
+
+// 32 parity bits -> 32 int8 bytes (nbits = 32 or 16) at a 16-B aligned address
+__device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits) {
+    uint4 a = make_uint4(expand4(bits & 15u), expand4((bits >> 4) & 15u), expand4((bits >> 8) & 15u),
+                         expand4((bits >> 12) & 15u));
+    *(uint4*)dst = a;
+    if (nbits > 16) {
+        uint4 b = make_uint4(expand4((bits >> 16) & 15u), expand4((bits >> 20) & 15u),
+                             expand4((bits >> 24) & 15u), expand4(bits >> 28));
+        *(uint4*)(dst + 16) = b;
+    }
+}
+
+template <int BG>
+__global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
+                                                            int8_t* __restrict__ dn, int B, int Zc,
+                                                            int zi, int64_t ldk, int64_t ldn) {
+    using P = BGT<BG>;
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int t = threadIdx.x;
+    const int NT = blockDim.x;
+    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
+    const int K = Ly.K, W = Ly.W, DW = Ly.DW, KW = Ly.KW;
+    const int twoZ = 2 * Zc;
+    const int S = K - twoZ;
+    extern __shared__ __align__(16) uint32_t sm[];
+    uint32_t* ib = sm;
+    uint32_t* X = ib + KW + 2;
+    uint32_t* lam = X + P::KC * DW;
+    uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
+    const int8_t* src = ck + (int64_t)b * ldk;
+    int8_t* dst = dn + (int64_t)b * ldn;
+
+    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn
+    for (int wi = t; wi < KW; wi += NT) {
+        const int base = wi * 32;   // K = Kb*Zc is a multiple of 32 when Zc % 16 == 0
+        uint32_t bits = 0;
+        if (base + 32 <= K) {
+            int4 v[2];
+            v[0] = *(const int4*)(src + base);
+            v[1] = *(const int4*)(src + base + 16);
+            if (base >= twoZ) {   // 2Zc and K are multiples of 32 here
+                *(int4*)(dst + base - twoZ) = v[0];
+                *(int4*)(dst + base - twoZ + 16) = v[1];
+            }
+            const uint32_t* d = (const uint32_t*)v;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t x = d[q];
+                // per byte: LSB, minus fillers (0xff) at positions >= 2Zc
+                uint32_t lsb = x & 0x01010101u;
+                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                                     (x >> 6) & (x >> 7)) & 0x01010101u;   // byte == 0xff
+                if (base + 4 * q >= twoZ) lsb &= ~ff;
+                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+            }
+        } else {   // (unreachable for Kb*Zc % 32 == 0; kept for safety)
+            int4 v0 = *(const int4*)(src + base);
+            if (base >= twoZ) *(int4*)(dst + base - twoZ) = v0;
+            const uint32_t* d = (const uint32_t*)&v0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = d[q];
+                uint32_t lsb = x & 0x01010101u;
+                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                                     (x >> 6) & (x >> 7)) & 0x01010101u;
+                if (base + 4 * q >= twoZ) lsb &= ~ff;
+                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+            }
+        }
+        ib[wi] = bits;
+    }
+    if (t < 2) ib[KW + t] = 0;
+    __syncthreads();
+
+    // ---- 2. periodic extensions of the information columns
+    for (int task = t; task < P::KB * DW; task += NT) {
+        int j = task / DW, q = task - j * DW;
+        X[j * DW + q] = fetch_rot32(ib, j * Zc, Zc, mod_zc(32 * q, Zc));
+    }
+    __syncthreads();
+
+    // ---- 3+4. lambda and the double-diagonal recursion, all inside wave 0
+    constexpr int eS = (BG == 1) ? edge_of<BG>(1, 22) : edge_of<BG>(2, 10);
+    constexpr int eA = edge_of<BG>(0, P::KB);
+    constexpr int eC = edge_of<BG>(3, P::KB);
+    constexpr int eD = (BG == 1) ? edge_of<BG>(2, 25) : edge_of<BG>(1, 11);
+    uint32_t* p1 = pv;
+    uint32_t* p2 = pv + W;
+    uint32_t* p3 = pv + 2 * W;
+    uint32_t* p4 = pv + 3 * W;
+    uint32_t* L2 = pv + 4 * W;
+    if (t < 64) {
+        for (int task = t; task < 4 * W; task += 64) {
+            int i = task / W, w = task - i * W;
+            uint32_t acc = 0;
+            for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+                int j = col_d<BG>(e);
+                if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+            }
+            lam[i * W + w] = acc;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) L2[w] = lam[w] ^ lam[W + w] ^ lam[2 * W + w] ^ lam[3 * W + w];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int s1 = shift_of<BG>(zi, eS);
+        for (int w = t; w < W; w += 64)
+            p1[w] = fetch_rot32(L2, 0, Zc, mod_zc(mod_zc(32 * w, Zc) + Zc - s1, Zc));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) {
+            p2[w] = lam[w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eA), Zc));
+            p4[w] = lam[3 * W + w] ^ fetch_rot32(p1, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eC), Zc));
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (int w = t; w < W; w += 64) {
+            if constexpr (BG == 1) p3[w] = lam[2 * W + w] ^ fetch_rot32(p4, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+            else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
+        }
+    }
+    __syncthreads();
+
+    // ---- 5. extensions of the 4 core parity columns; core parity bytes straight to dn
+    for (int task = t; task < 4 * DW; task += NT) {
+        int k = task / DW, q = task - k * DW;
+        X[(P::KB + k) * DW + q] = fetch_rot32(pv + k * W, 0, Zc, mod_zc(32 * q, Zc));
+    }
+    for (int task = t; task < 4 * W; task += NT) {
+        int k = task / W, w = task - k * W;
+        store_bits(dst + S + k * Zc + 32 * w, pv[k * W + w], min(32, Zc - 32 * w));
+    }
+    __syncthreads();
+
+    // ---- 6. extension parity rows, each row-word stored straight to dn
+    for (int task = t; task < (P::MB - 4) * W; task += NT) {
+        int i = 4 + task / W, w = task % W;
+        uint32_t acc = 0;
+        for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
+            int j = col_d<BG>(e);
+            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+        }
+        store_bits(dst + S + i * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+    }
+}
+
+}  // namespace
+
+int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,
+                  int64_t ldn, hipStream_t st) {
+    const bool fast = (Zc % 16) == 0 && (ldk % 16) == 0 && (ldn % 16) == 0 &&
+                      (((uintptr_t)ck) & 15) == 0 && (((uintptr_t)dn) & 15) == 0;
+    if (fast) {
+        static const int nt = [] {
+            const char* e = getenv("LDPC5G_ENC_THREADS");
+            int v = e ? atoi(e) : 128;
+            return (v == 64 || v == 128 || v == 256) ? v : 128;
+        }();
+        if (bgn == 1)
+            hipLaunchKernelGGL(ldpc_enc_fast_kernel<1>, dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
+                               st, ck, dn, B, Zc, zi, ldk, ldn);
+        else
+            hipLaunchKernelGGL(ldpc_enc_fast_kernel<2>, dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
+                               st, ck, dn, B, Zc, zi, ldk, ldn);
+        return check_hip(hipGetLastError(), "ldpc_enc_fast_kernel launch");
+    }
+    if (bgn == 1)
+        hipLaunchKernelGGL(ldpc_enc_kernel<1>, dim3(B), dim3(256), enc_lds_bytes<1>(Zc), st, ck, dn,
+                           B, Zc, zi, ldk, ldn);
+    else
+        hipLaunchKernelGGL(ldpc_enc_kernel<2>, dim3(B), dim3(256), enc_lds_bytes<2>(Zc), st, ck, dn,
+                           B, Zc, zi, ldk, ldn);
+    return check_hip(hipGetLastError(), "ldpc_enc_kernel launch");
+}
+
+}  // namespace ldpc5g_impl

@@ -12,8 +12,10 @@ Precision / parity
     arithmetic (numpy float64), so ck and status are bit-identical to the reference.
   * The batched API takes float32 LLRs by default (the bench path): flooding float32 is the same
     algorithm rounded to fp32; 'layered' is the faster row-serial schedule.
-  * algo='BP' / 'BF' are accepted by the reference's assert but have no GPU kernel yet: they
-    raise NotImplementedError (no silent CPU fallback).
+  * algo='BF' runs the GPU bit-flipping kernel (ldpc_decoder_bit_flipping.py:5-73) — bit-exact,
+    ck returned as float64 like the reference; algo='BP' runs the float64 sum-product flooding
+    kernel (_BP_process :145-176) — the GPU's tanh/atanh are not numpy's, so BP matches the
+    reference's status and decisions to within transcendental rounding.
 """
 import numpy as np
 
@@ -25,10 +27,6 @@ SCHEDULES = {"flooding": _lib.FLOODING, "layered": _lib.LAYERED}
 
 def _check_algo(algo):
     assert algo in ["BF", "BP", "min-sum"]
-    if algo != "min-sum":
-        raise NotImplementedError(
-            f"algo='{algo}' has no GPU kernel in this build (min-sum family only: MS/NMS/OMS/"
-            "mixed via alpha/beta); see DESIGN.md §7")
 
 
 def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
@@ -65,11 +63,27 @@ def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
         it = t.empty((B,), dtype=t.int32, device=x.device)
     else:
         ck, st, it = out
+    flags = _lib.LLR_FULL if full else 0
+    lib = _lib.lib()
     with t.cuda.device(x.device):
-        _lib.check(_lib.lib().ldpc5g_decode_ms(
-            _lib.ptr(x), dt, _lib.ptr(ck), _lib.ptr(st), _lib.ptr(it), B, bgn, Zc, int(L),
-            float(alpha), float(beta), SCHEDULES[schedule], _lib.LLR_FULL if full else 0,
-            x.stride(0), ck.stride(0), _lib.stream_ptr(x.device)))
+        stream = _lib.stream_ptr(x.device)
+        if algo == "min-sum":
+            _lib.check(lib.ldpc5g_decode_ms(
+                _lib.ptr(x), dt, _lib.ptr(ck), _lib.ptr(st), _lib.ptr(it), B, bgn, Zc, int(L),
+                float(alpha), float(beta), SCHEDULES[schedule], flags, x.stride(0), ck.stride(0),
+                stream))
+        elif algo == "BF":
+            _lib.check(lib.ldpc5g_decode_bf(
+                _lib.ptr(x), dt, _lib.ptr(ck), _lib.ptr(st), _lib.ptr(it), B, bgn, Zc, int(L),
+                flags, x.stride(0), ck.stride(0), stream))
+        else:   # BP: float64 sum-product with a per-edge message scratch
+            if x.dtype != t.float64:
+                x = x.double()
+            n = lib.ldpc5g_bp_scratch_elems(B, bgn, Zc)
+            scratch = t.empty((max(n, 1),), dtype=t.float64, device=x.device)
+            _lib.check(lib.ldpc5g_decode_bp(
+                _lib.ptr(x), _lib.ptr(ck), _lib.ptr(st), _lib.ptr(it), _lib.ptr(scratch), n, B,
+                bgn, Zc, int(L), flags, x.stride(0), ck.stride(0), stream))
     if is_np:
         return ck.cpu().numpy(), st.cpu().numpy().astype(bool), it.cpu().numpy()
     return ck, st, it
@@ -91,6 +105,8 @@ def nr_decode_ldpc(LLRin, Zc, bgn, L, algo="min-sum", alpha=1, beta=0):
     ck, st, _ = nr_decode_ldpc_batch(np.asarray(LLRin, np.float64).reshape(1, N), Zc, bgn, L,
                                      algo, alpha, beta, "flooding")
     ck = ck[0]
+    if algo == "BF":
+        ck = ck.astype(np.float64)   # the reference's BF decisions are a float copy of LLRin
     return ck[0:K], ck, bool(st[0])
 
 
@@ -107,7 +123,8 @@ def decode_ldpc(LLRin, H, L, algo="min-sum", alpha=1, beta=0):
     bgn, Zc = m
     ck, st, _ = nr_decode_ldpc_batch(np.asarray(LLRin, np.float64).reshape(1, Ncol), Zc, bgn, L,
                                      algo, alpha, beta, "flooding", full=True)
-    return ck[0], bool(st[0])
+    ck = ck[0].astype(np.float64) if algo == "BF" else ck[0]
+    return ck, bool(st[0])
 
 
 def for_test_5g_ldpc_encoder(Zc, bgn, snr_db, crcpoly="24A"):

@@ -53,6 +53,20 @@ def load_decode_cases():
     return out
 
 
+def load_algo_cases(algo):
+    """[dict(bg, Zc, L, llr float32[N], ck int8[Nf], status)] — reference nr_decode_ldpc with
+    algo='BF' / 'BP' (tests/golden/decode_{bf,bp}_golden.npz)."""
+    d = np.load(os.path.join(GOLD, f"decode_{algo.lower()}_golden.npz"))
+    out = []
+    for i in range(d["bg"].size):
+        bg, Zc = int(d["bg"][i]), int(d["Zc"][i])
+        Nf = (68 if bg == 1 else 52) * Zc
+        out.append(dict(bg=bg, Zc=Zc, L=int(d["L"][i]),
+                        llr=d["llr"][d["llr_off"][i]:d["llr_off"][i + 1]],
+                        ck=_unpack(d["ck_bits"], d["ck_off"], i, Nf), status=bool(d["status"][i])))
+    return out
+
+
 def load_json(name):
     with open(os.path.join(GOLD, name)) as f:
         return json.load(f)

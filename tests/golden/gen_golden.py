@@ -15,6 +15,7 @@ the float64 widening of those float32 values so the fixtures are exact for both 
   ratematch_golden.npz ratematch_ldpc / raterecover_ldpc / get_k0 / get_Er cases
   crc_golden.json      CRC KATs (the inline vectors of py5gphy/crc/crc.py:167-210) + generated
   dlsch_golden.npz     DLSCHEncode (nr_dlsch.py:12) transport blocks -> g_seq
+  decode_bf_golden.npz / decode_bp_golden.npz   nr_decode_ldpc with algo='BF' / 'BP'
 """
 import json
 import multiprocessing as mp
@@ -196,6 +197,43 @@ def gen_decode(pool):
     print("decode cases", len(cases), "status True", sum(r[1] for r in res))
 
 
+# ------------------------------------------------------------------------------ BF / BP
+def _decode_algo_case(args):
+    (bg, Zc, L, algo, llr32) = args
+    _, dec = _ref()
+    t = time.time()
+    _, ck, status = dec.nr_decode_ldpc(llr32.astype(np.float64), Zc, bg, L, algo, 1, 0)
+    return np.packbits(np.asarray(ck) != 0), bool(status), time.time() - t
+
+
+def gen_bf_bp(pool):
+    """nr_decode_ldpc(..., algo='BF') (ldpc_decoder_bit_flipping.py:5-73) and algo='BP'
+    (nr_ldpc_decode.py:145-176) on small lifting sizes."""
+    rng = np.random.default_rng(123)
+    cases = []
+    for algo, snrs in (("BF", [3.0, 4.0, 5.0, 6.0]), ("BP", [-1.0, 0.0, 1.0, 2.0])):
+        for n in range(40):
+            bg = 1 + n % 2
+            Zc = [2, 3, 5, 7, 9, 11, 13, 15, 8, 12, 20, 26, 36, 40][n % 14]
+            snr = snrs[n % 4]
+            L = [8, 16][(n // 4) % 2]
+            cases.append((algo, bg, Zc, L, _mk_awgn(rng, bg, Zc, snr)))
+    t = time.time()
+    res = pool.map(_decode_algo_case, [(c[1], c[2], c[3], c[0], c[4]) for c in cases], chunksize=1)
+    print("bf/bp decode done", time.time() - t)
+    for algo in ("BF", "BP"):
+        idx = [k for k, c in enumerate(cases) if c[0] == algo]
+        np.savez_compressed(
+            os.path.join(OUT, f"decode_{algo.lower()}_golden.npz"),
+            bg=np.array([cases[k][1] for k in idx], np.int32),
+            Zc=np.array([cases[k][2] for k in idx], np.int32),
+            L=np.array([cases[k][3] for k in idx], np.int32),
+            llr=np.concatenate([cases[k][4] for k in idx]), llr_off=_offs([cases[k][4] for k in idx]),
+            ck_bits=np.concatenate([res[k][0] for k in idx]), ck_off=_offs([res[k][0] for k in idx]),
+            status=np.array([res[k][1] for k in idx]))
+        print(algo, "cases", len(idx), "status True", sum(res[k][1] for k in idx))
+
+
 # --------------------------------------------------------------------------- rate matching
 def gen_ratematch():
     from py5gphy.ldpc import ldpc_info, nr_ldpc_ratematch as RM, nr_ldpc_raterecover as RR
@@ -284,7 +322,7 @@ def gen_dlsch():
 if __name__ == "__main__":
     os.chdir(REF)
     sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
-    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "decode"]
+    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "decode", "bfbp"]
     if "encode" in which:
         gen_encode()
     if "crc" in which:
@@ -296,3 +334,6 @@ if __name__ == "__main__":
     if "decode" in which:
         with mp.get_context("fork").Pool(6) as pool:
             gen_decode(pool)
+    if "bfbp" in which:
+        with mp.get_context("fork").Pool(6) as pool:
+            gen_bf_bp(pool)

@@ -13,7 +13,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import load_decode_cases
+from conftest import load_algo_cases, load_decode_cases
 from oracle import ldpc_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -258,8 +258,8 @@ def test_decode_errors_are_assertions(torch, dec):
         dec.nr_decode_ldpc(np.zeros(66 * 8), 8, 3, 8)
     with pytest.raises(AssertionError):
         dec.nr_decode_ldpc(np.zeros(66 * 8 + 1), 8, 1, 8)
-    with pytest.raises(NotImplementedError):
-        dec.nr_decode_ldpc(np.zeros(66 * 8), 8, 1, 8, "BP")
+    with pytest.raises(AssertionError):
+        dec.nr_decode_ldpc(np.zeros(66 * 8), 8, 1, 8, "LDPC")
 
 
 def test_dlsch_encode_chain_with_gpu_encoder(torch, enc):
@@ -284,3 +284,50 @@ def test_dlsch_encode_chain_with_gpu_encoder(torch, enc):
             k0 = RM.get_k0(Ncb, bgn, rv, Zc)
             out.append(RM.ratematch_ldpc(dn, Ncb, Er[c], k0, Qm))
         assert np.array_equal(np.concatenate(out), g_ref)
+
+
+# ---------------------------------------------------------------------------------- BF / BP
+def test_decode_bf_golden_bitexact(torch, dec):
+    """algo='BF' (ldpc_decoder_bit_flipping.py:5-73): ck (float64 like the reference) and status
+    bit-exact on all 40 golden cases; batched kernel == oracle incl. iteration counts."""
+    cases = load_algo_cases("BF")
+    for c in cases:
+        blk, ck, st = dec.nr_decode_ldpc(c["llr"].astype(np.float64), c["Zc"], c["bg"], c["L"], "BF")
+        assert ck.dtype == np.float64 and np.array_equal(ck, c["ck"]) and st == c["status"]
+    for (bg, Zc, L), cs in _groups3(cases).items():
+        llr = np.stack([c["llr"] for c in cs]).astype(np.float64)
+        got = dec.nr_decode_ldpc_batch(llr, Zc, bg, L, "BF")
+        ref = O.decode_bf(llr, Zc, bg, L)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r)
+
+
+def _groups3(cases):
+    g = {}
+    for c in cases:
+        g.setdefault((c["bg"], c["Zc"], c["L"]), []).append(c)
+    return g
+
+
+def test_decode_bp_golden(torch, dec):
+    """algo='BP' (float64 sum-product, _BP_process :145-176): the GPU's tanh/atanh are not
+    numpy's, so messages differ in the last ulps.  Bar: identical status on every golden case,
+    identical ck whenever the reference decoded successfully."""
+    for c in load_algo_cases("BP"):
+        blk, ck, st = dec.nr_decode_ldpc(c["llr"].astype(np.float64), c["Zc"], c["bg"], c["L"], "BP")
+        assert ck.dtype == np.int8 and st == c["status"], (c["bg"], c["Zc"], c["L"])
+        if c["status"]:
+            assert np.array_equal(ck, c["ck"]), (c["bg"], c["Zc"])
+
+
+def test_decode_bp_batch_vs_oracle(torch, dec):
+    rng = np.random.default_rng(9)
+    for bg, Zc in [(1, 13), (2, 36)]:
+        K = (22 if bg == 1 else 10) * Zc
+        ck = rng.integers(0, 2, (64, K)).astype(np.int8)
+        llr = O.bpsk_awgn_llr(O.encode(ck, bg), 1.0, rng)
+        got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 12, "BP")
+        ref = O.decode_bp(llr, Zc, bg, 12)
+        assert np.array_equal(got[1], ref[1])
+        both = ref[1]
+        assert np.array_equal(got[0][both], ref[0][both]) and np.array_equal(got[2][both], ref[2][both])

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, load_json
+from conftest import GOLD, load_algo_cases, load_json
 from oracle import ldpc_oracle as O
 
 
@@ -143,3 +143,13 @@ def test_dlsch_encode_chain_golden():
             k0 = O.get_k0(Ncb, bgn, rv, Zc)
             out.append(O.ratematch(dn[c], Ncb, Er[c], k0, Qm))
         assert np.array_equal(np.concatenate(out), g_ref)
+
+
+@pytest.mark.parametrize("algo", ["BF", "BP"])
+def test_bf_bp_golden(algo):
+    """decode_bf / decode_bp restatements == reference nr_decode_ldpc(algo='BF'/'BP'), bit for
+    bit (the BP restatement uses numpy's own tanh/arctanh, like the reference)."""
+    fn = O.decode_bf if algo == "BF" else O.decode_bp
+    for c in load_algo_cases(algo):
+        ck, st, _ = fn(c["llr"][None].astype(np.float64), c["Zc"], c["bg"], c["L"])
+        assert np.array_equal(ck[0], c["ck"]) and bool(st[0]) == c["status"], (c["bg"], c["Zc"])
