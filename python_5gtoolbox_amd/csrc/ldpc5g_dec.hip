@@ -41,6 +41,14 @@ __device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, uint32_t idx, int k
     return FT<T>::xsign((idx == (uint32_t)k) ? mB : mA, pk << (31 - k));
 }
 
+// Layered state: mA/mB carry the row sign (product of all q signs), pk bits d-1-k hold the sign
+// of q_k (packed with v_alignbit, edge 0 highest), bits 24..28 the argmin edge.  Then
+// r_k = (k == idx ? mB : mA) with its sign flipped by sign(q_k) — the same value as decomp().
+template <typename T>
+__device__ __forceinline__ T decomp_l(T mAs, T mBs, uint32_t pk, uint32_t idx, int d, int k) {
+    return FT<T>::xsign((idx == (uint32_t)k) ? mBs : mAs, pk << (32 - d + k));
+}
+
 // Consecutive base rows with disjoint core columns form one barrier group: processing them
 // together is identical to processing them one after another (layered) and keeps the
 // row-ascending accumulation order of every column (flooding).  BG1: 46 rows -> 32 groups,
@@ -94,7 +102,7 @@ __device__ __forceinline__ uint32_t shift_word(int zi, int w) {
 template <typename T, bool LAYERED>
 constexpr size_t dec_lds_bytes_t(int MB, int KC) {
     return (size_t)KC * kCS * sizeof(T) * (LAYERED ? 1 : 2) +
-           (sizeof(T) == 4 ? (size_t)(MB - 4) * kCS * sizeof(T) : 0) + 2 * kCS * sizeof(int);
+           (sizeof(T) == 4 ? (size_t)(MB - 4) * kCS * sizeof(T) : 0) + (2 * kCS + 4) * sizeof(int);
 }
 
 template <int BG, typename T, bool LAYERED>
@@ -113,15 +121,19 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
     constexpr int FLAG_B = XL_B + (XL_LDS ? (MB - 4) * kCS * TS : 0);
     extern __shared__ __align__(16) unsigned char smem[];
 
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
     int Zc = Zc_u, zi = zi_u, G = G_u;
     const int t = threadIdx.x;
     if (work) {
         DecWork w = work[blockIdx.x];
         Zc = w.Zc, zi = w.zi, G = w.G;
     }
-    const int cbl = t / Zc;
-    const int z = t - cbl * Zc;
-    bool valid = cbl < G;
+    // thread t = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
+    // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
+    const int z = t / G;
+    const int cbl = t - z * G;
+    bool valid = z < Zc;
     const T* lrow = llr;
     int8_t* crow = ck;
     int out = 0;
@@ -140,13 +152,29 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         }
     }
     const int cl = valid ? cbl : 0;
-    const int tzb = (cl * Zc + z) * TS;   // byte offset of this thread's own column entry
-    const int ZcT = Zc * TS;
+    const int tzb = valid ? t * TS : 0;   // byte offset of this thread's own column entry
+    const uint32_t GT = (uint32_t)(G * TS), ZGT = (uint32_t)(Zc * G * TS);
+    const uint32_t tzbw = (uint32_t)tzb - ZGT;   // own entry one wrap back (negative -> huge)
     int zv = z, ziv = zi;   // made opaque per iteration (see the iteration loop)
     int* flagA = (int*)(smem + FLAG_B);
     int* flagB = flagA + kCS;
-    auto at = [&](int byte) -> T& { return *(T*)(smem + byte); };
-    auto own = [&](int j) -> T& { return at(j * kCS * TS + tzb); };
+    // block-wide "any": the slot holds the epoch of the last call in which some thread voted yes.
+    // No reset is needed; consecutive calls are separated by other barriers.  (__syncthreads_or
+    // would pull in 256 B of static LDS, moving the dynamic base off 0 and costing a v_add per
+    // edge address.)
+    int* anyf = flagB + kCS;
+    int epoch = 0;
+    auto block_any = [&](bool p) -> bool {
+        ++epoch;
+        if (p) *anyf = epoch;
+        __syncthreads();
+        return *anyf == epoch;
+    };
+    // LDS is addressed by plain byte offsets: this kernel has no static LDS, so the dynamic block
+    // starts at LDS address 0 (checked at entry) and no symbol base is added to every address.
+    using lds_T = __attribute__((address_space(3))) T;
+    auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
+    auto own = [&](int j) -> lds_T& { return at(j * kCS * TS + tzb); };
     // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
     auto llrx = [&](int i4) -> T {
         if constexpr (XL_LDS) return at(XL_B + i4 * kCS * TS + tzb);
@@ -175,11 +203,17 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         }
     }
     if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+    if (t == 0) *anyf = 0;
     bool active = valid;
     __syncthreads();
 
     // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
-    auto rot = [&](int s) -> int { return tzb + s * TS - (zv >= Zc - s ? ZcT : 0); };
+    // ((z + s) mod Zc, cl): the unwrapped candidate is tzb + s*GT; when z + s >= Zc the wrapped
+    // one tzbw + s*GT is a valid (smaller) offset, otherwise it is negative, i.e. a huge unsigned.
+    auto rot = [&](int s) -> int {
+        const uint32_t S = (uint32_t)s * GT;
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
 
     int it = 0;
     for (; it < L; ++it) {
@@ -191,6 +225,107 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         asm volatile("" : "+s"(ziv));
         bool fail = false;
         uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
+        // ---- flooding row i (reference order, nr_ldpc_decode.py:117-131)
+        auto flooding_row = [&](auto ic, auto& gshift) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            const T mA = sA[i], mB = sB[i];
+            const uint32_t pk = sP[i];
+            const uint32_t idxo = pk >> 24;
+            T q[d];
+            int rb[d];
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0;
+            bool par = false;
+            // pass 1: variable-to-check messages q = LQ - Lr, two-min, sign product
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const T rold = decomp(mA, mB, pk, idxo, k);
+                T a;
+                if constexpr (j < KC) {
+                    rb[k] = rot(gshift(e0 + k));
+                    a = at(j * kCS * TS + rb[k]);
+                } else {
+                    a = llrx(i - 4) + rold;   // LQ of a degree-1 column
+                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                }
+                par ^= a < T(0);
+                const T qq = a - rold;
+                q[k] = qq;
+                const T aq = fabs(qq);
+                idx = aq < min1 ? (uint32_t)k : idx;
+                negs |= (FT<T>::sbits(qq) >> 31) << k;
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
+                sx ^= FT<T>::sbits(qq);
+            });
+            fail |= par;
+            const T x1 = min1 - beta, x2 = min2 - beta;
+            const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
+            const T nB = alpha * (x2 > T(0) ? x2 : T(0));
+            // pass 2: Lr = sign * (k == argmin ? nB : nA), accumulated row-ascending (:126)
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
+                    const T r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
+                    lds_T& acc = at(ACC_B + j * kCS * TS + rb[k]);
+                    acc = acc + r;
+                }
+            });
+            sA[i] = nA;
+            sB[i] = nB;
+            sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
+        };
+        // ---- layered row i: q = APP - r_old, APP = q + r_new
+        auto layered_row = [&](auto ic, auto& gshift) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            const T mAs = sA[i], mBs = sB[i];
+            const uint32_t pk = sP[i];
+            const uint32_t idxo = pk >> 24;
+            T q[d];
+            int rb[d];
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    rb[k] = rot(gshift(e0 + k));
+                    q[k] = at(j * kCS * TS + rb[k]) - decomp_l(mAs, mBs, pk, idxo, d, k);
+                } else {
+                    q[k] = llrx(i - 4);   // degree-1 column: q is the channel LLR itself
+                }
+                const T aq = fabs(q[k]);
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
+                sx ^= FT<T>::sbits(q[k]);
+            });
+            const T x1 = min1 - beta, x2 = min2 - beta;
+            const T nAs = FT<T>::xsign(alpha * (x1 > T(0) ? x1 : T(0)), sx);
+            const T nBs = FT<T>::xsign(alpha * (x2 > T(0) ? x2 : T(0)), sx);
+            uint32_t negs = 0, idxn = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const uint32_t qb = FT<T>::sbits(q[k]);
+                const bool isMin = fabs(q[k]) == min1;   // ties: nB == nA, either is right
+                idxn = isMin ? (uint32_t)k : idxn;
+                const T r = FT<T>::xsign(isMin ? nBs : nAs, qb);
+                negs = __builtin_amdgcn_alignbit(negs, qb, 31);
+                const T app = q[k] + r;
+                if constexpr (j < KC) at(j * kCS * TS + rb[k]) = app;
+                else hdx |= (uint64_t)(app < T(0)) << (i - 4);
+            });
+            sA[i] = nAs;
+            sB[i] = nBs;
+            sP[i] = negs | (idxn << 24);
+        };
         // the next row group's packed shift words are loaded (scalar, wave-uniform) before the
         // barrier that precedes the group, so their latency hides behind it
         constexpr int NPW = max_group_nw<BG>();
@@ -214,82 +349,8 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
             };
             if (active) {
                 sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    constexpr int e0 = P::RS[i];
-                    constexpr int d = P::RS[i + 1] - e0;
-                    const T mA = sA[i], mB = sB[i];
-                    const uint32_t pk = sP[i];
-                    const uint32_t idxo = pk >> 24;
-                    T q[d];
-                    int rb[d];
-                    T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-                    uint32_t sx = 0, idx = 0, negs = 0;
-                    bool par = false;
-                    // ---- pass 1: variable-to-check messages q, two-min, sign product
-                    sfor<0, d>([&](auto kc) {
-                        constexpr int k = decltype(kc)::value;
-                        constexpr int j = P::COL[e0 + k];
-                        const T rold = decomp(mA, mB, pk, idxo, k);
-                        T qq;
-                        if constexpr (j < KC) {
-                            rb[k] = rot(gshift(e0 + k));
-                            const T a = at(j * kCS * TS + rb[k]);
-                            qq = a - rold;
-                            if constexpr (!LAYERED) par ^= a < T(0);
-                        } else if constexpr (LAYERED) {
-                            qq = llrx(i - 4);   // degree-1 column: q is the channel LLR itself
-                        } else {
-                            const T a = llrx(i - 4) + rold;   // LQ of a degree-1 column
-                            qq = a - rold;
-                            const bool h = a < T(0);
-                            par ^= h;
-                            hdx |= (uint64_t)h << (i - 4);
-                        }
-                        q[k] = qq;
-                        const T aq = fabs(qq);
-                        if constexpr (!LAYERED) {
-                            idx = aq < min1 ? (uint32_t)k : idx;
-                            negs |= (FT<T>::sbits(qq) >> 31) << k;
-                        }
-                        min2 = FT<T>::med3(min1, min2, aq);
-                        min1 = fmin(min1, aq);
-                        sx ^= FT<T>::sbits(qq);
-                    });
-                    fail |= par;
-                    const T x1 = min1 - beta, x2 = min2 - beta;
-                    const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
-                    const T nB = alpha * (x2 > T(0) ? x2 : T(0));
-                    // ---- pass 2: check-to-variable messages r = sign * (k == argmin ? nB : nA)
-                    uint32_t signs = 0, idxn = 0;
-                    sfor<0, d>([&](auto kc) {
-                        constexpr int k = decltype(kc)::value;
-                        constexpr int j = P::COL[e0 + k];
-                        T r;
-                        if constexpr (LAYERED) {
-                            const T aq = fabs(q[k]);
-                            const bool isMin = aq == min1;   // ties: nB == nA, either is right
-                            idxn = isMin ? (uint32_t)k : idxn;
-                            const uint32_t sb = FT<T>::sbits(q[k]) ^ sx;
-                            r = FT<T>::xsign(isMin ? nB : nA, sb);
-                            signs |= (sb >> 31) << k;
-                            if constexpr (j < KC) {
-                                at(j * kCS * TS + rb[k]) = q[k] + r;
-                            } else {
-                                hdx |= (uint64_t)(llrx(i - 4) + r < T(0)) << (i - 4);
-                            }
-                        } else {
-                            const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
-                            r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
-                            if constexpr (j < KC) {
-                                T& a = at(ACC_B + j * kCS * TS + rb[k]);
-                                a = a + r;   // row-ascending accumulation (:126)
-                            }
-                        }
-                    });
-                    sA[i] = nA;
-                    sB[i] = nB;
-                    if constexpr (LAYERED) sP[i] = signs | (idxn << 24);
-                    else sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
+                    if constexpr (LAYERED) layered_row(ic, gshift);
+                    else flooding_row(ic, gshift);
                 });
             }
             if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
@@ -309,7 +370,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                 active = false;
             } else if (active) {
                 for (int j = 0; j < KC; ++j) {
-                    T& acc = at(ACC_B + j * kCS * TS + tzb);
+                    lds_T& acc = at(ACC_B + j * kCS * TS + tzb);
                     const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
                     own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
                     acc = T(0);
@@ -326,7 +387,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
             hdx_prev = hdx;
             __syncthreads();
             const bool cand = active && flagA[cl] == 0;
-            if (__syncthreads_or(cand)) {
+            if (block_any(cand)) {
                 if (cand) {
                     bool sf = false;
                     sfor<0, MB>([&](auto ic) {
@@ -358,9 +419,14 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         }
         __syncthreads();
         if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
-        if (!__syncthreads_or(active)) break;
+        if (!block_any(active)) break;
     }
 
+    // r of edge k of row i from the stored state (layout depends on the schedule)
+    auto rfinal = [&](int i, int d, int k) -> T {
+        if constexpr (LAYERED) return decomp_l(sA[i], sB[i], sP[i], sP[i] >> 24, d, k);
+        else return decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
+    };
     // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
     zv = z;
     asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
@@ -376,7 +442,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
                 constexpr int j = P::COL[e0 + k];
                 T a;
                 if constexpr (j < KC) a = at(j * kCS * TS + rot(shift_of<BG>(zi, e0 + k)));
-                else a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
+                else a = llrx(i - 4) + rfinal(i, d, k);
                 par ^= (a <= T(0));
             });
             fail |= par;
@@ -389,7 +455,7 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(
         sfor<4, MB>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
-            const T a = llrx(i - 4) + decomp(sA[i], sB[i], sP[i], sP[i] >> 24, dl);
+            const T a = llrx(i - 4) + rfinal(i, dl + 1, dl);
             crow[(KB + i) * Zc + zv] = (int8_t)(a <= T(0));
         });
         if (z == 0) {

@@ -50,7 +50,7 @@ def main():
                    torch.empty((B,), dtype=torch.int32, device="cuda"))
             ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, 1, 8, "min-sum", 0.75, 0.0, what,
                                                        out=out), 5)
-            print(f"{what} B={B}: {ms:.3f} ms  {B / ms / 1e3:.1f} k CB/s  iters "
+            print(f"{what} B={B}: {ms:.3f} ms  {B / ms / 1e3:.3f} M CB/s  iters "
                   f"{out[2].float().mean().item():.2f}")
 
 
