@@ -112,6 +112,10 @@ const char* ldpc5g_last_error(void);
 /* Library version string. */
 const char* ldpc5g_version(void);
 
+/* Diagnostics: decoder workgroups that can be resident on one CU (HIP occupancy calculator) for
+ * (bgn, llr_dtype, schedule).  No reference counterpart. */
+int ldpc5g_dec_blocks_per_cu(int32_t bgn, int32_t llr_dtype, int32_t schedule);
+
 #ifdef __cplusplus
 }
 #endif

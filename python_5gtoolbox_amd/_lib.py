@@ -16,8 +16,10 @@ EBGN, EZC, ESIZE, EHIP = -1, -2, -3, -4
 
 # every symbol include/ldpc5g.h declares: name -> (restype, argtypes)
 _c = ctypes
+OPTIONAL = {"ldpc5g_dec_blocks_per_cu"}
 SIGNATURES = {
     "ldpc5g_find_ils": (_c.c_int, [_c.c_int32]),
+    "ldpc5g_dec_blocks_per_cu": (_c.c_int, [_c.c_int32, _c.c_int32, _c.c_int32]),
     "ldpc5g_encode": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_int32, _c.c_int32,
                                  _c.c_int64, _c.c_int64, _c.c_void_p]),
     "ldpc5g_decode_ms": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
@@ -63,6 +65,8 @@ def lib():
                 "(there is no CPU fallback for the LDPC hot path)")
         h = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in OPTIONAL and not hasattr(h, name):
+                continue   # diagnostics absent from an older library (A/B builds)
             f = getattr(h, name)
             f.restype = res
             f.argtypes = args

@@ -1,6 +1,9 @@
 """Build libldpc5g.so (gfx950) in-tree with hipcc.
 
-    python -m python_5gtoolbox_amd.build [--force]
+    python -m python_5gtoolbox_amd.build [--force] [--csrc DIR --out LIB]
+
+(--csrc/--out build an alternative source tree into another library, for A/B timing on one GPU
+box via LDPC5G_LIB=...; the default build is the in-tree one.)
 
 Each csrc/*.hip translation unit is compiled to an object in parallel, then linked into
 python_5gtoolbox_amd/libldpc5g.so, which travels with the repo snapshot to the GPU box.
@@ -22,6 +25,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
          "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
 
+# v_pk_add_f32 issues at ~1/3 the rate of two scalar v_add_f32 on gfx950 (tools/abl/opbench2.hip),
+# so the decoder TU is built without the SLP vectorizer that forms it.
+NO_SLP = {"ldpc5g_dec.hip"}
+
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
@@ -38,31 +45,42 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
-def _compile(src, verbose):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+def _compile(src, verbose, obj_dir=None, csrc=CSRC):
+    obj = os.path.join(obj_dir or OBJ, os.path.basename(src) + ".o")
+    flags = [f for f in FLAGS if f != f"-I{CSRC}"] + [f"-I{csrc}"]
+    if os.path.basename(src) in NO_SLP:
+        flags.append("-fno-slp-vectorize")
+    cmd = [HIPCC, *flags, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     return obj
 
 
-def build(force=False, verbose=True):
-    if not force and up_to_date():
+def build(force=False, verbose=True, csrc=None, out=None):
+    alt = csrc is not None
+    lib_path = out or LIB
+    if not alt and not force and up_to_date():
         if verbose:
             print("libldpc5g.so up to date")
         return LIB
-    os.makedirs(OBJ, exist_ok=True)
-    srcs = sources()
+    csrc = csrc or CSRC
+    obj_dir = os.path.join(ROOT, "build", "obj_alt" if alt else "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
-    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+        objs = list(ex.map(lambda s: _compile(s, verbose, obj_dir, csrc), srcs))
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib_path + ".tmp"]
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.run(link, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib_path + ".tmp", lib_path)
+    return lib_path
+
+
+def _arg(name):
+    return sys.argv[sys.argv.index(name) + 1] if name in sys.argv else None
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, csrc=_arg("--csrc"), out=_arg("--out"))

@@ -56,6 +56,12 @@ extern "C" {
 
 const char* ldpc5g_version(void) { return LDPC5G_VERSION; }
 
+// Diagnostics (not part of the drop-in surface): decoder workgroups resident per CU.
+int ldpc5g_dec_blocks_per_cu(int32_t bgn, int32_t llr_dtype, int32_t schedule) {
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn=%d", bgn);
+    return dec_blocks_per_cu(bgn, llr_dtype, schedule == LDPC5G_LAYERED);
+}
+
 const char* ldpc5g_last_error(void) { return g_err.c_str(); }
 
 int ldpc5g_find_ils(int32_t Zc) {
@@ -153,7 +159,7 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
     if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
     if (B == 0) return LDPC5G_OK;
     if (!desc || !llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
-    // group codeblocks by (bgn, Zc), pack G = floor(384/Zc) per workgroup
+    // group codeblocks by (bgn, Zc), pack G = floor(threads/Zc) per workgroup
     std::vector<std::vector<int>> bucket[2];
     bucket[0].resize(LDPC5G_NUM_ZC);
     bucket[1].resize(LDPC5G_NUM_ZC);
@@ -170,7 +176,7 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
     for (int g = 0; g < 2; ++g)
         for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
             const std::vector<int>& v = bucket[g][zi];
-            const int Zc = kLdpcZcList[zi], G = dec_G(Zc);
+            const int Zc = kLdpcZcList[zi], G = dec_G(Zc, schedule == LDPC5G_LAYERED);
             for (size_t s = 0; s < v.size(); s += G) {
                 DecWork w;
                 w.zi = zi, w.Zc = Zc, w.G = (int)std::min<size_t>(G, v.size() - s), w.first = (int)refs.size();

@@ -85,7 +85,14 @@ struct CbRef {       // one codeblock of the mixed-Zc path
 constexpr int kDecThreads = 384;   // = max Zc: one thread per check row z of a base row
 constexpr int kCS = kDecThreads;   // LDS column stride (entries): G*Zc <= 384 always
 
-inline int dec_G(int Zc) { return Zc >= kDecThreads ? 1 : kDecThreads / Zc; }
+// layered float32 kernel: 768-thread workgroups (12 waves = 3 per SIMD at <= 168 VGPRs) holding
+// G = floor(768 / Zc) codeblocks, e.g. two BG1 Zc=384 codeblocks
+constexpr int kDecThreadsL = 768;
+inline int dec_threads(bool layered) { return layered ? kDecThreadsL : kDecThreads; }
+inline int dec_G(int Zc, bool layered = false) {
+    const int T = dec_threads(layered);
+    return Zc >= T ? 1 : T / Zc;
+}
 
 // ---- host helpers (ldpc5g_capi.hip)
 int fail(int code, const char* fmt, ...);
@@ -95,6 +102,8 @@ int check_hip(hipError_t e, const char* what);
 // ---- launchers (one per translation unit)
 int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,
                   int64_t ldn, hipStream_t st);
+// workgroups of the decoder kernel resident per CU (HIP occupancy calculator), diagnostics
+int dec_blocks_per_cu(int bgn, int dtype, bool layered);
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
                double alpha, double beta, int pc, hipStream_t st);

@@ -13,7 +13,10 @@ import torch  # noqa: E402
 
 from python_5gtoolbox_amd import nr_ldpc_decode as D, nr_ldpc_encode as E  # noqa: E402
 
-ZC, K, N, NF = 384, 22 * 384, 66 * 384, 68 * 384
+BG = int(os.environ.get("PROBE_BG", "1"))
+ZC = 384
+K, N, NF = ((22, 66, 68) if BG == 1 else (10, 50, 52))
+K, N, NF = K * ZC, N * ZC, NF * ZC
 
 
 def timeit(fn, reps):
@@ -30,6 +33,13 @@ def timeit(fn, reps):
 
 def main():
     what = sys.argv[1]
+    if what == "occupancy":
+        from python_5gtoolbox_amd import _lib
+        lib = _lib.lib()
+        for bg in (1, 2):
+            for name, dt, sch in (("f64 flooding", 0, 0), ("f32 flooding", 1, 0), ("f32 layered", 1, 1)):
+                print(f"BG{bg} {name}: {lib.ldpc5g_dec_blocks_per_cu(bg, dt, sch)} workgroups/CU")
+        return
     sizes = [int(x) for x in sys.argv[2:]] or [4096]
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
@@ -37,18 +47,18 @@ def main():
         ck = torch.randint(0, 2, (B, K), dtype=torch.int8, device="cuda", generator=g)
         if what == "encode":
             dn = torch.empty((B, N), dtype=torch.int8, device="cuda")
-            ms = timeit(lambda: E.encode_ldpc_batch(ck, 1, out=dn), 50)
+            ms = timeit(lambda: E.encode_ldpc_batch(ck, BG, out=dn), 50)
             print(f"encode B={B}: {ms * 1e3:.1f} us  {B / ms / 1e3:.1f} M CB/s  "
                   f"{B * (K + N) / ms / 1e6:.0f} GB/s")
         else:
-            dn = E.encode_ldpc_batch(ck, 1)
+            dn = E.encode_ldpc_batch(ck, BG)
             sigma = 10 ** (3.0 / 20)
             llr = (2 * ((1 - 2 * dn.float()) + sigma * torch.randn(dn.shape, device="cuda",
                                                                      generator=g)) / sigma ** 2)
             out = (torch.empty((B, NF), dtype=torch.int8, device="cuda"),
                    torch.empty((B,), dtype=torch.uint8, device="cuda"),
                    torch.empty((B,), dtype=torch.int32, device="cuda"))
-            ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, 1, 8, "min-sum", 0.75, 0.0, what,
+            ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, BG, 8, "min-sum", 0.75, 0.0, what,
                                                        out=out), 5)
             print(f"{what} B={B}: {ms:.3f} ms  {B / ms / 1e3:.3f} M CB/s  iters "
                   f"{out[2].float().mean().item():.2f}")
