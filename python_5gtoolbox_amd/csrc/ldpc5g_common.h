@@ -104,6 +104,14 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
                   int64_t ldn, hipStream_t st);
 // workgroups of the decoder kernel resident per CU (HIP occupancy calculator), diagnostics
 int dec_blocks_per_cu(int bgn, int dtype, bool layered);
+// layered float32 instantiations (ldpc5g_dec_l.hip)
+int dec_blocks_per_cu_l(int bgn);
+int launch_dec_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
+                 int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                 hipStream_t st);
+int launch_dec_mixed_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                       int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
+                       double beta, int pc, hipStream_t st);
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
                double alpha, double beta, int pc, hipStream_t st);

@@ -1,0 +1,680 @@
+// ldpc5g_dec_body.h — flooding / layered min-sum decoder kernels (py5gphy/ldpc/nr_ldpc_decode.py:
+// 11-143, 178-227), included by ldpc5g_dec.hip (flooding instantiations) and ldpc5g_dec_l.hip
+// (layered instantiations).  The two translation units are compiled with different vectorizer
+// settings (build.py NO_SLP): SLP-formed v_pk_add_f32 helps the flooding kernel and hurts the
+// layered one.  Reference mapping in ldpc5g_common.h / DESIGN.md §4.
+#pragma once
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "ldpc5g_common.h"
+
+namespace ldpc5g_impl {
+namespace {
+// ================================================================================== DECODER
+template <typename T>
+struct FT;
+template <>
+struct FT<float> {
+    __device__ static __forceinline__ uint32_t sbits(float x) { return __float_as_uint(x); }
+    // x with its sign bit XORed by bit 31 of `b`
+    __device__ static __forceinline__ float xsign(float x, uint32_t b) {
+        return __uint_as_float(__float_as_uint(x) ^ (b & 0x80000000u));
+    }
+    __device__ static __forceinline__ float inf() { return __uint_as_float(0x7f800000u); }
+    __device__ static __forceinline__ float med3(float a, float b, float c) {
+        return __builtin_amdgcn_fmed3f(a, b, c);
+    }
+};
+template <>
+struct FT<double> {
+    __device__ static __forceinline__ uint32_t sbits(double x) { return (uint32_t)__double2hiint(x); }
+    __device__ static __forceinline__ double xsign(double x, uint32_t b) {
+        return __longlong_as_double(__double_as_longlong(x) ^ ((long long)(b & 0x80000000u) << 32));
+    }
+    __device__ static __forceinline__ double inf() { return __longlong_as_double(0x7ff0000000000000ll); }
+    __device__ static __forceinline__ double med3(double a, double b, double c) {
+        return fmax(fmin(a, b), fmin(fmax(a, b), c));
+    }
+};
+
+template <typename T>
+using V2 = T __attribute__((ext_vector_type(2)));
+
+// Compressed check-node state of one row: r_k = (k == idx ? mB : mA), sign = bit k of pk.
+// pk: bits 0..deg-1 = sign of r_k, bits 24..28 = idx (an edge holding min |q|).
+template <typename T>
+__device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, uint32_t idx, int k) {
+    return FT<T>::xsign((idx == (uint32_t)k) ? mB : mA, pk << (31 - k));
+}
+
+// Layered state: mA/mB carry the row sign (product of all q signs), pk bits d-1-k hold the sign
+// of q_k (packed with v_alignbit, edge 0 highest), bits 24..28 the argmin edge.  Then
+// r_k = (k == idx ? mB : mA) with its sign flipped by sign(q_k) — the same value as decomp().
+template <typename T>
+__device__ __forceinline__ T decomp_l(T mAs, T mBs, uint32_t pk, uint32_t idx, int d, int k) {
+    return FT<T>::xsign((idx == (uint32_t)k) ? mBs : mAs, pk << (32 - d + k));
+}
+
+// Consecutive base rows with disjoint core columns form one barrier group: processing them
+// together is identical to processing them one after another (layered) and keeps the
+// row-ascending accumulation order of every column (flooding).  BG1: 46 rows -> 32 groups,
+// BG2: 42 -> 28.
+template <int BG>
+struct RowGroups {
+    int n = 0;
+    int start[64] = {};
+    constexpr RowGroups() {
+        using P = BGT<BG>;
+        int g0 = 0;
+        start[0] = 0;
+        n = 1;
+        for (int i = 1; i < P::MB; ++i) {
+            bool dis = true;
+            for (int a = g0; a < i && dis; ++a)
+                for (int e = P::RS[a]; e < P::RS[a + 1]; ++e)
+                    for (int f = P::RS[i]; f < P::RS[i + 1]; ++f)
+                        if (P::COL[e] == P::COL[f] && P::COL[e] < P::KC) dis = false;
+            if (!dis) {
+                start[n++] = i;
+                g0 = i;
+            }
+        }
+        start[n] = P::MB;
+    }
+};
+template <int BG>
+constexpr RowGroups<BG> kGroups{};
+
+// Packed shift words (2 edges per word) spanned by the edges of row group g.
+template <int BG>
+constexpr int group_w0(int g) { return BGT<BG>::RS[kGroups<BG>.start[g]] >> 1; }
+template <int BG>
+constexpr int group_nw(int g) {
+    return ((BGT<BG>::RS[kGroups<BG>.start[g + 1]] - 1) >> 1) - group_w0<BG>(g) + 1;
+}
+template <int BG>
+constexpr int max_group_nw() {
+    int m = 0;
+    for (int g = 0; g < kGroups<BG>.n; ++g) m = m > group_nw<BG>(g) ? m : group_nw<BG>(g);
+    return m;
+}
+template <int BG>
+__device__ __forceinline__ uint32_t shift_word(int zi, int w) {
+    if constexpr (BG == 1) return kBG1ShiftMod[zi][w];
+    else return kBG2ShiftMod[zi][w];
+}
+
+
+// Ext (degree-1) column LLRs are staged in LDS only by the float32 flooding kernel; the layered
+// kernel reads them from global memory one row group ahead, which keeps its LDS at ~40 KB so two
+// workgroups (12 waves, 3 per SIMD) share a CU.
+template <typename T, bool LAYERED>
+constexpr bool xl_lds() { return sizeof(T) == 4 && !LAYERED; }
+
+// Layered: the (mA, mB) magnitudes of the first kLdsRows rows live in LDS rather than VGPRs, so
+// the kernel fits the 168-VGPR budget of 3 waves/SIMD without scratch spills (spilling kernels
+// are held to fewer resident waves).  2 x (40 KB APP + 33 KB state + 3 KB flags) <= 160 KB.
+template <int BG>
+constexpr int lds_rows() { return BG == 1 ? 11 : 18; }
+// LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
+template <bool LAYERED>
+constexpr int dec_cs() { return LAYERED ? kDecThreadsL : kDecThreads; }
+constexpr int kMaxG = kDecThreadsL / 2;   // = 768 / min Zc (2): per-CB-slot flag entries
+
+template <int BG, typename T, bool LAYERED>
+constexpr size_t dec_lds_bytes_t() {
+    constexpr size_t CS = dec_cs<LAYERED>();
+    return (size_t)BGT<BG>::KC * CS * sizeof(T) * (LAYERED ? 1 : 2) +
+           (xl_lds<T, LAYERED>() ? (size_t)(BGT<BG>::MB - 4) * CS * sizeof(T) : 0) +
+           (LAYERED ? (size_t)2 * lds_rows<BG>() * CS * sizeof(T) : 0) + (2 * kMaxG + 4) * sizeof(int);
+}
+
+// Layered state words: rows 0..3 one word each (negs | idx << 24); rows >= 4 (degree <= 12) two
+// 16-bit fields (negs | idx << 12) per word.
+template <int BG>
+constexpr bool ext_rows_fit16() {
+    for (int i = 4; i < BGT<BG>::MB; ++i)
+        if (BGT<BG>::RS[i + 1] - BGT<BG>::RS[i] > 12) return false;
+    return true;
+}
+template <int BG>
+constexpr int max_group_ext_rows() {
+    int m = 0;
+    for (int g = 0; g < kGroups<BG>.n; ++g) {
+        int c = 0;
+        for (int i = kGroups<BG>.start[g]; i < kGroups<BG>.start[g + 1]; ++i) c += i >= 4;
+        m = m > c ? m : c;
+    }
+    return m;
+}
+
+// Workgroup barrier that orders LDS only.  Threads of the decoder never exchange data through
+// global memory, and __syncthreads()'s global release would make every barrier wait (vmcnt(0))
+// for the ext-LLR loads prefetched across it.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int BG, typename T, bool LAYERED>
+__device__ __forceinline__ void dec_body(
+    const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
+    int L, T alpha, T beta, int pc, const DecWork* __restrict__ work,
+    const CbRef* __restrict__ cbs) {
+    // pc = number of leading punctured block columns absent from the LLR rows (2, or 0 when the
+    // caller passes full-length rows as decode_ldpc(LLRin, H, ...) does, nr_ldpc_decode.py:51)
+    using P = BGT<BG>;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
+    constexpr int CS = dec_cs<LAYERED>();   // LDS column stride = workgroup size
+    constexpr bool XL_LDS = xl_lds<T, LAYERED>();
+    static_assert(!LAYERED || ext_rows_fit16<BG>(), "packed layered state needs degree <= 12");
+    constexpr int ACC_B = KC * CS * TS;                        // byte offsets in LDS
+    constexpr int XL_B = KC * CS * TS * (LAYERED ? 1 : 2);
+    constexpr int ST_B = XL_B + (XL_LDS ? (MB - 4) * CS * TS : 0);   // layered: LDS row state
+    constexpr int NLR = LAYERED ? lds_rows<BG>() : 0;
+    constexpr int FLAG_B = ST_B + 2 * NLR * CS * TS;
+    extern __shared__ __align__(16) unsigned char smem[];
+
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
+    int Zc = Zc_u, zi = zi_u, G = G_u;
+    const int t = threadIdx.x;
+    if (work) {
+        DecWork w = work[blockIdx.x];
+        Zc = w.Zc, zi = w.zi, G = w.G;
+    }
+    // thread t = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
+    // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
+    const int z = t / G;
+    const int cbl = t - z * G;
+    bool valid = z < Zc;
+    const T* lrow = llr;
+    int8_t* crow = ck;
+    int out = 0;
+    if (valid) {
+        if (work) {
+            CbRef r = cbs[work[blockIdx.x].first + cbl];
+            lrow = llr + r.llr_off;
+            crow = ck + r.ck_off;
+            out = r.out;
+        } else {
+            int cb = blockIdx.x * G + cbl;
+            valid = cb < B;
+            lrow = llr + (int64_t)cb * ldl;
+            crow = ck + (int64_t)cb * ldc;
+            out = cb;
+        }
+    }
+    const int cl = valid ? cbl : 0;
+    const int tzb = valid ? t * TS : 0;   // byte offset of this thread's own column entry
+    const uint32_t GT = (uint32_t)(G * TS), ZGT = (uint32_t)(Zc * G * TS);
+    const uint32_t tzbw = (uint32_t)tzb - ZGT;   // own entry one wrap back (negative -> huge)
+    // global row index used in the iteration loop: threads outside any CB (z >= Zc or cb >= B)
+    // use row 0 of CB 0, so loads issued without a branch stay in bounds
+    const int zg = valid ? z : 0;
+    int zv = zg, ziv = zi;   // made opaque per iteration (see the iteration loop)
+    int* flagA = (int*)(smem + FLAG_B);
+    int* flagB = flagA + kMaxG;
+    // block-wide "any": the slot holds the epoch of the last call in which some thread voted yes.
+    // No reset is needed; consecutive calls are separated by other barriers.  (__syncthreads_or
+    // would pull in 256 B of static LDS, moving the dynamic base off 0 and costing a v_add per
+    // edge address.)
+    int* anyf = flagB + kMaxG;
+    int epoch = 0;
+    auto block_any = [&](bool p) -> bool {
+        ++epoch;
+        if (p) *anyf = epoch;
+        lds_barrier();
+        return *anyf == epoch;
+    };
+    // LDS is addressed by plain byte offsets: this kernel has no static LDS, so the dynamic block
+    // starts at LDS address 0 (checked at entry) and no symbol base is added to every address.
+    using lds_T = __attribute__((address_space(3))) T;
+    auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
+    auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
+    // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
+    auto llrx = [&](int i4) -> T {
+        if constexpr (XL_LDS) return at(XL_B + i4 * CS * TS + tzb);
+        else return lrow[(KB + 4 + i4 - pc) * Zc + zv];
+    };
+
+    // per-thread state of rows (i, z), i = 0..MB-1
+    constexpr int NSP = LAYERED ? 4 + (MB - 3) / 2 : MB;
+    T sA[MB], sB[MB];
+    uint32_t sP[NSP];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) sA[i] = T(0), sB[i] = T(0);
+    // (mA, mB) of row i: VGPRs, or LDS for the first NLR rows of the layered kernel
+    auto getA = [&](auto ic) -> T {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NLR) return at(ST_B + (2 * i) * CS * TS + tzb);
+        else return sA[i];
+    };
+    auto getB = [&](auto ic) -> T {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NLR) return at(ST_B + (2 * i + 1) * CS * TS + tzb);
+        else return sB[i];
+    };
+    auto putAB = [&](auto ic, T a, T b) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NLR) {
+            at(ST_B + (2 * i) * CS * TS + tzb) = a;
+            at(ST_B + (2 * i + 1) * CS * TS + tzb) = b;
+        } else {
+            sA[i] = a;
+            sB[i] = b;
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < NSP; ++i) sP[i] = 0u;
+    // layered: row i's sign bits / argmin as one word (negs | idx << 24), whatever the storage
+    auto get_row = [&](auto ic) -> uint32_t {
+        constexpr int i = decltype(ic)::value;
+        constexpr int d = P::RS[i + 1] - P::RS[i];
+        if constexpr (!LAYERED || i < 4) {
+            return sP[i];
+        } else {
+            constexpr int w = 4 + (i - 4) / 2;
+            const uint32_t f = ((i - 4) & 1) ? (sP[w] >> 16) : (sP[w] & 0xffffu);
+            return (f & ((1u << d) - 1u)) | ((f >> 12) << 24);
+        }
+    };
+    auto put_row = [&](auto ic, uint32_t negs, uint32_t idx) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (!LAYERED || i < 4) {
+            sP[i] = negs | (idx << 24);
+        } else {
+            constexpr int w = 4 + (i - 4) / 2;
+            const uint32_t f = negs | (idx << 12);
+            sP[w] = ((i - 4) & 1) ? ((sP[w] & 0xffffu) | (f << 16)) : ((sP[w] & 0xffff0000u) | f);
+        }
+    };
+
+    uint32_t hdc_prev = 0;   // layered: hard decisions of own core columns, last iteration end
+    uint64_t hdx_prev = 0;   // layered: ... of own extension columns
+    if (valid) {
+        for (int j = 0; j < KC; ++j) {
+            const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
+            own(j) = v;
+            if (!LAYERED) at(ACC_B + j * CS * TS + tzb) = T(0);
+            hdc_prev |= (uint32_t)(v < T(0)) << j;
+        }
+        for (int i4 = 0; i4 < MB - 4; ++i4) {
+            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            if constexpr (XL_LDS) at(XL_B + i4 * CS * TS + tzb) = v;
+            hdx_prev |= (uint64_t)(v < T(0)) << i4;
+        }
+    }
+    for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);
+    if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+    if (t == 0) *anyf = 0;
+    bool active = valid;
+    lds_barrier();
+
+    // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
+    // ((z + s) mod Zc, cl): the unwrapped candidate is tzb + s*GT; when z + s >= Zc the wrapped
+    // one tzbw + s*GT is a valid (smaller) offset, otherwise it is negative, i.e. a huge unsigned.
+    auto rot = [&](int s) -> int {
+        const uint32_t S = (uint32_t)s * GT;
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
+
+    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
+    asm volatile("" : "+v"(mv));
+    int it = 0;
+    for (; it < L; ++it) {
+        // zv / ziv are re-materialised opaque each iteration: otherwise LICM hoists the ~300
+        // loop-invariant column addresses (z + V) mod Zc out of the loop into VGPRs/SGPRs.
+        zv = zg;
+        ziv = zi;
+        asm volatile("" : "+v"(zv));
+        asm volatile("" : "+s"(ziv));
+        bool fail = false;
+        uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
+        // ---- flooding row i (reference order, nr_ldpc_decode.py:117-131)
+        auto flooding_row = [&](auto ic, auto& gshift) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            const T mA = sA[i], mB = sB[i];
+            const uint32_t pk = sP[i];
+            const uint32_t idxo = pk >> 24;
+            T q[d];
+            int rb[d];
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0;
+            bool par = false;
+            // pass 1: variable-to-check messages q = LQ - Lr, two-min, sign product
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const T rold = decomp(mA, mB, pk, idxo, k);
+                T a;
+                if constexpr (j < KC) {
+                    rb[k] = rot(gshift(e0 + k));
+                    a = at(j * CS * TS + rb[k]);
+                } else {
+                    a = llrx(i - 4) + rold;   // LQ of a degree-1 column
+                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                }
+                par ^= a < T(0);
+                const T qq = a - rold;
+                q[k] = qq;
+                const T aq = fabs(qq);
+                idx = aq < min1 ? (uint32_t)k : idx;
+                negs |= (FT<T>::sbits(qq) >> 31) << k;
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
+                sx ^= FT<T>::sbits(qq);
+            });
+            fail |= par;
+            const T x1 = min1 - beta, x2 = min2 - beta;
+            const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
+            const T nB = alpha * (x2 > T(0) ? x2 : T(0));
+            // pass 2: Lr = sign * (k == argmin ? nB : nA), accumulated row-ascending (:126)
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
+                    const T r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
+                    lds_T& acc = at(ACC_B + j * CS * TS + rb[k]);
+                    acc = acc + r;
+                }
+            });
+            sA[i] = nA;
+            sB[i] = nB;
+            sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
+        };
+        // ---- layered row i: q = APP - r_old, APP = q + r_new.
+        //      Op choice follows the gfx950 VALU rates measured by tools/microbench/valu_rates.hip: f32
+        //      add/sub and all-VGPR bitwise ops (and, xor, bitop3, u32 add) issue at twice the
+        //      rate of min/max/med3, compares and any op with an SGPR or literal operand.  So the
+        //      sign mask lives in a VGPR (mv) and the sign bits are walked with u + u.
+        auto layered_row = [&](auto ic, auto& gshift, T xl) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            const T mAs = getA(ic), mBs = getB(ic);
+            const uint32_t pk = get_row(ic);
+            const uint32_t idxo = pk >> 24;
+            uint32_t u = pk << (32 - d);   // bit 31 = sign of q_k for the edge k being visited
+            T q[d];
+            int rb[d];
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    rb[k] = rot(gshift(e0 + k));
+                    const T sel = (idxo == (uint32_t)k) ? mBs : mAs;
+                    const T rold = __uint_as_float(__builtin_amdgcn_bitop3_b32(u, __float_as_uint(sel), mv, 0x6c));
+                    q[k] = at(j * CS * TS + rb[k]) - rold;
+                } else {
+                    q[k] = xl;   // degree-1 column: q is the channel LLR itself
+                }
+                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
+                const T aq = fabs(q[k]);
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
+                if constexpr (k % 2 == 1)   // three-input XOR
+                    sx = __builtin_amdgcn_bitop3_b32(sx, FT<T>::sbits(q[k - 1]), FT<T>::sbits(q[k]), 0x96);
+                else if constexpr (k == d - 1)
+                    sx ^= FT<T>::sbits(q[k]);
+            });
+            const T x1 = min1 - beta, x2 = min2 - beta;
+            const T nAs = FT<T>::xsign(alpha * (x1 > T(0) ? x1 : T(0)), sx);
+            const T nBs = FT<T>::xsign(alpha * (x2 > T(0) ? x2 : T(0)), sx);
+            uint32_t negs = 0, idxn = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const uint32_t qb = FT<T>::sbits(q[k]);
+                const bool isMin = fabs(q[k]) == min1;   // ties: nB == nA, either is right
+                idxn = isMin ? (uint32_t)k : idxn;
+                const T sel = isMin ? nBs : nAs;
+                const T r = __uint_as_float(__builtin_amdgcn_bitop3_b32(qb, __float_as_uint(sel), mv, 0x6c));
+                negs = __builtin_amdgcn_alignbit(negs, qb, 31);
+                const T app = q[k] + r;
+                if constexpr (j < KC) at(j * CS * TS + rb[k]) = app;
+                else hdx |= (uint64_t)(app < T(0)) << (i - 4);
+            });
+            putAB(ic, nAs, nBs);
+            put_row(ic, negs, idxn);
+        };
+        // the next row group's packed shift words are loaded (scalar, wave-uniform) before the
+        // barrier that precedes the group, so their latency hides behind it
+        constexpr int NPW = max_group_nw<BG>();
+        constexpr int NXR = max_group_ext_rows<BG>() > 0 ? max_group_ext_rows<BG>() : 1;
+        uint32_t nsw[NPW];
+        T xlb[2][NXR] = {};   // layered: ext-column LLRs of rows >= 4, double-buffered by group parity
+        auto prefetch = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            sfor<0, group_nw<BG>(g)>([&](auto wc) {
+                constexpr int w = decltype(wc)::value;
+                nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
+            });
+        };
+        // layered: the ext-column LLRs of group g are loaded from global memory at the start of
+        // group g - 1, so a whole group's work hides the L2 / Infinity-Cache latency
+        auto prefetch_xl = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (LAYERED) {
+                constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
+                sfor<r0, (kGroups<BG>.start[g + 1] > r0 ? kGroups<BG>.start[g + 1] : r0)>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];   // unconditional: see zg
+                });
+            }
+        };
+        prefetch(std::integral_constant<int, 0>{});
+        prefetch_xl(std::integral_constant<int, 0>{});   // row 0 has no ext column: no load
+        sfor<0, kGroups<BG>.n>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
+            if constexpr (g + 1 < kGroups<BG>.n) prefetch_xl(std::integral_constant<int, g + 1>{});
+            auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
+                return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+            };
+            if (active) {
+                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
+                    if constexpr (LAYERED) layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));
+                    else flooding_row(ic, gshift);
+                });
+            }
+            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
+            lds_barrier();
+        });
+
+        if constexpr (!LAYERED) {
+            // ---- reference order: the syndrome of LQ at the start of the pass decides (:107-114)
+            if (active && fail) flagA[cl] = 1;
+            lds_barrier();
+            const bool conv = active && flagA[cl] == 0;
+            if (conv) {
+                for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
+                for (int i4 = 0; i4 < MB - 4; ++i4)
+                    crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
+                if (z == 0) status[out] = 1, iters[out] = it;
+                active = false;
+            } else if (active) {
+                for (int j = 0; j < KC; ++j) {
+                    lds_T& acc = at(ACC_B + j * CS * TS + tzb);
+                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
+                    own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
+                    acc = T(0);
+                }
+            }
+        } else {
+            // ---- layered stopping rule: no hard decision changed over the iteration, then an
+            //      exact syndrome check of those decisions (oracle.decode_layered)
+            uint32_t hdc = 0;
+            if (active)
+                for (int j = 0; j < KC; ++j) hdc |= (uint32_t)(own(j) < T(0)) << j;
+            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;
+            hdc_prev = hdc;
+            hdx_prev = hdx;
+            lds_barrier();
+            const bool cand = active && flagA[cl] == 0;
+            if (block_any(cand)) {
+                if (cand) {
+                    bool sf = false;
+                    sfor<0, MB>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        constexpr int e0 = P::RS[i];
+                        constexpr int d = P::RS[i + 1] - e0;
+                        bool par = false;
+                        sfor<0, d>([&](auto kc) {
+                            constexpr int k = decltype(kc)::value;
+                            constexpr int j = P::COL[e0 + k];
+                            if constexpr (j < KC)
+                                par ^= at(j * CS * TS + rot(shift_of<BG>(ziv, e0 + k))) < T(0);
+                            else
+                                par ^= (bool)((hdx >> (i - 4)) & 1u);
+                        });
+                        sf |= par;
+                    });
+                    if (sf) flagB[cl] = 1;
+                }
+                lds_barrier();
+                if (cand && flagB[cl] == 0) {
+                    for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)((hdc >> j) & 1u);
+                    for (int i4 = 0; i4 < MB - 4; ++i4)
+                        crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
+                    if (z == 0) status[out] = 1, iters[out] = it + 1;
+                    active = false;
+                }
+            }
+        }
+        lds_barrier();
+        if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+        if (!block_any(active)) break;
+    }
+
+    // r of edge k of row i from the stored state (layout depends on the schedule)
+    auto rfinal = [&](auto ic, int d, int k) -> T {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (LAYERED) {
+            const uint32_t pk = get_row(ic);
+            return decomp_l(getA(ic), getB(ic), pk, pk >> 24, d, k);
+        } else {
+            return decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
+        }
+    };
+    // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
+    zv = z;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    if (active) {
+        bool fail = false;
+        sfor<0, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                T a;
+                if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                else a = llrx(i - 4) + rfinal(ic, d, k);
+                par ^= (a <= T(0));
+            });
+            fail |= par;
+        });
+        if (fail) flagA[cl] = 1;
+    }
+    lds_barrier();
+    if (active) {
+        for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+        sfor<4, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+            const T a = llrx(i - 4) + rfinal(ic, dl + 1, dl);
+            crow[(KB + i) * Zc + zv] = (int8_t)(a <= T(0));
+        });
+        if (z == 0) {
+            status[out] = flagA[cl] == 0;
+            iters[out] = L;
+        }
+    }
+}
+
+#define LDPC5G_DEC_PARAMS                                                                        \
+    const T *__restrict__ llr, int8_t *__restrict__ ck, uint8_t *__restrict__ status,             \
+        int32_t *__restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc, \
+        int L, T alpha, T beta, int pc, const DecWork *__restrict__ work,                          \
+        const CbRef *__restrict__ cbs
+#define LDPC5G_DEC_ARGS \
+    llr, ck, status, iters, B, Zc_u, zi_u, G_u, ldl, ldc, L, alpha, beta, pc, work, cbs
+
+// flooding (float64 / float32): one workgroup per CU (VGPR-bound)
+template <int BG, typename T, bool LAYERED>
+__global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(LDPC5G_DEC_PARAMS) {
+    dec_body<BG, T, LAYERED>(LDPC5G_DEC_ARGS);
+}
+// layered float32: 768 threads = 12 waves = 3 per SIMD (<= 168 VGPRs), G = floor(768/Zc) CBs
+template <int BG, typename T, bool LAYERED>
+__global__ __launch_bounds__(kDecThreadsL) __attribute__((amdgpu_waves_per_eu(3))) void
+ldpc_dec_kernel_l(LDPC5G_DEC_PARAMS) {
+    dec_body<BG, T, LAYERED>(LDPC5G_DEC_ARGS);
+}
+template <int BG, typename T, bool LAYERED>
+constexpr auto dec_kernel() {
+    if constexpr (LAYERED) return ldpc_dec_kernel_l<BG, T, LAYERED>;
+    else return ldpc_dec_kernel<BG, T, LAYERED>;
+}
+
+template <int BG, typename T, bool LAYERED>
+size_t dec_lds_bytes() {
+    static_assert(dec_lds_bytes_t<BG, T, LAYERED>() <= 160 * 1024, "LDS budget of one CU");
+    return dec_lds_bytes_t<BG, T, LAYERED>();
+}
+
+template <int BG, typename T, bool LAYERED>
+int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                 int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    auto kern = dec_kernel<BG, T, LAYERED>();
+    const int G = dec_G(Zc, LAYERED);
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
+    const int threads = ((G * Zc + 63) / 64) * 64;
+    const int grid = (B + G - 1) / G;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, llr, ck, status, iters, B, Zc, zi,
+                       G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
+                       (const CbRef*)nullptr);
+    return check_hip(hipGetLastError(), "ldpc_dec_kernel launch");
+}
+
+template <int BG, typename T, bool LAYERED>
+int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                       const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
+                       int pc, hipStream_t st) {
+    auto kern = dec_kernel<BG, T, LAYERED>();
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(dec_cs<LAYERED>()), lds, st, llr, ck, status, iters, 0, 0,
+                       0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
+    return check_hip(hipGetLastError(), "ldpc_dec_kernel(mixed) launch");
+}
+
+template <int BG, typename T, bool LAYERED>
+int blocks_per_cu_t() {
+    auto kern = dec_kernel<BG, T, LAYERED>();
+    const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int n = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, dec_cs<LAYERED>(), lds) != hipSuccess) return -1;
+    return n;
+}
+
+}  // namespace
+}  // namespace ldpc5g_impl
