@@ -106,6 +106,92 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
                            int32_t L, double alpha, double beta, int32_t schedule,
                            int32_t flags, void* stream);
 
+/* ============================================================ DL-SCH / UL-SCH transport chain
+ * TS 38.212 §7.2 (DL-SCH) / §6.2 (UL-SCH) around the codec, batched over T transport blocks that
+ * share one configuration.  Bits are int8 0/1 (fillers -1); CRC remainders are uint32 with the
+ * first CRC bit in bit L-1.  */
+
+/* CRC generator ids (py5gphy/crc/crc.py:94-106) */
+#define LDPC5G_CRC6 0
+#define LDPC5G_CRC11 1
+#define LDPC5G_CRC16 2
+#define LDPC5G_CRC24A 3
+#define LDPC5G_CRC24B 4
+#define LDPC5G_CRC24C 5
+
+/* CRC of `rows` bit rows ([rows][ld] int8, nbits each): rem[r] = M(x) x^L mod g(x), the parity
+ * nr_crc_encode appends (crc.py:4-41, mask 0, bit L-1 first); a row that ends in its own CRC gives
+ * 0 iff nr_crc_decode reports no error (crc.py:43-88).  rem must not alias bits. */
+int ldpc5g_crc(const int8_t* bits, int64_t ld, int64_t nbits, int32_t rows, int32_t poly,
+               uint32_t* rem, void* stream);
+
+/* Shared-configuration geometry of a transport block (host struct, filled by ldpc5g_sch_config). */
+typedef struct {
+    int32_t A;            /* TBSize                                                           */
+    int32_t B;            /* A + TB CRC length                                                */
+    int32_t tb_crc_poly;  /* LDPC5G_CRC24A (A > 3824) or LDPC5G_CRC16 (nr_dlsch.py:34-40)      */
+    int32_t bgn;          /* base graph (nr_dlsch.py:44-49)                                   */
+    int32_t C, cbz, Lcb, F, K, K_apo, Zc;   /* get_cbs_info (ldpc_info.py:5-78); K_apo = cbz+Lcb */
+    int32_t N, Ncb, k0;   /* codeword length, circular buffer (Nref / N), rv start             */
+    int32_t Qm, NL, rv;
+    int32_t E_lo, E_hi, c_switch;   /* Er: codeblocks c < c_switch get E_lo, the others E_hi    */
+    int64_t G;            /* the G that sized Er (nr_ldpc_ratematch.py:5-27)                   */
+    int64_t E_total;      /* sum of Er = bits of g per transport block                         */
+} ldpc5g_sch_cfg_t;
+
+/* Fill cfg for a transport block: TBSize A, modulation order Qm, code rate * 1024, layers NL,
+ * redundancy version rv, TBS_LBRM (> 0: DL-SCH limited buffer Nref = floor(TBS_LBRM / (2C/3)),
+ * nr_dlsch.py:63-65; 0: UL-SCH Ncb = N, nr_ulsch.py:55-58) and G (rate-matching output bits).
+ * Float arithmetic of the reference (base-graph thresholds, k0, Er) is reproduced in double. */
+int ldpc5g_sch_config(int32_t A, int32_t Qm, double coderateby1024, int32_t NL, int32_t rv,
+                      int64_t TBS_LBRM, int64_t G, ldpc5g_sch_cfg_t* cfg);
+
+/* DLSCHEncode (py5gphy/nr_pdsch/nr_dlsch.py:12-74) / ULSCH_Crc_CodeBlockSegment +
+ * ULSCH_encoding_ratematch (nr_pusch/nr_ulsch.py:13-70) of T transport blocks:
+ *   trblk [T][lda] int8 -> g [T][ldg] int8 (E_total bits each).
+ * Workspaces (device, caller-owned): ck [T*C][K] int8 (codeblocks with CRC24B and -1 fillers,
+ * as ldpc_cbsegment returns them), dn [T*C][N] int8 (encoder output), tb_crc [T] uint32 (the
+ * TB CRC, also an output). */
+int ldpc5g_sch_encode(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
+                      const ldpc5g_sch_cfg_t* cfg, int32_t T, int8_t* ck, int8_t* dn,
+                      uint32_t* tb_crc, void* stream);
+
+/* The two halves of ldpc5g_sch_encode:
+ *   ldpc5g_sch_segment   TB CRC + codeblock segmentation + CRC24B (nr_dlsch.py:32-56,
+ *                        ULSCH_Crc_CodeBlockSegment nr_ulsch.py:13-35): trblk -> ck, tb_crc
+ *   ldpc5g_sch_ratematch LDPC encode + rate matching + concatenation (nr_dlsch.py:58-74,
+ *                        ULSCH_encoding_ratematch nr_ulsch.py:37-70): ck -> dn -> g
+ * ldpc5g_sch_ratematch reads only the codeblock fields of cfg (bgn, C, cbz, Lcb, K, K_apo, Zc,
+ * N, Ncb, k0, Qm, E_lo, E_hi, c_switch). */
+int ldpc5g_sch_segment(const int8_t* trblk, int64_t lda, const ldpc5g_sch_cfg_t* cfg, int32_t T,
+                       int8_t* ck, uint32_t* tb_crc, void* stream);
+int ldpc5g_sch_ratematch(const int8_t* ck, const ldpc5g_sch_cfg_t* cfg, int32_t T, int8_t* dn,
+                         int8_t* g, int64_t ldg, void* stream);
+
+/* Rate recovery (nr_ldpc_raterecover.py:6-65) of every codeblock + optional HARQ combining with
+ * the previous decoder inputs (nr_dlsch_decode.py:73-88):
+ *   llr [T][ldg] (llr_dtype) -> llr_dn [T*C][N] (dn_dtype); harq_in NULL or [T*C][N] dn_dtype.
+ * Computed in float64 like the reference (a float32 llr_dn is the float64 result rounded once). */
+int ldpc5g_sch_raterecover(const void* llr, int32_t llr_dtype, int64_t ldg,
+                           const ldpc5g_sch_cfg_t* cfg, int32_t T, const void* harq_in,
+                           void* llr_dn, int32_t dn_dtype, void* stream);
+
+/* TB reassembly and CRC checks (nr_dlsch_decode.py:93-106): ck [T*C][ldc] int8 hard decisions
+ * -> tbblk [T][ldb] int8 (B = A + CRC bits: the TB and its CRC), cb_crc_ok [T*C] (CRC24B when
+ * C > 1, else 1), tb_ok [T] (TB CRC), tb_rem [T] uint32 (TB CRC remainder, scratch + output). */
+int ldpc5g_sch_tb_check(const int8_t* ck, int64_t ldc, const ldpc5g_sch_cfg_t* cfg, int32_t T,
+                        int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok, uint32_t* tb_rem,
+                        uint8_t* tb_ok, void* stream);
+
+/* DLSCHDecode (nr_dlsch_decode.py:13-110) / ULSCH_decoding (nr_ulsch_decode.py:13-110) with the
+ * min-sum decoder: ldpc5g_sch_raterecover -> ldpc5g_decode_ms over the T*C codeblocks (ck
+ * [T*C][Nf], status / iters [T*C]) -> ldpc5g_sch_tb_check.  Asynchronous on `stream`. */
+int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldpc5g_sch_cfg_t* cfg,
+                      int32_t T, const void* harq_in, void* llr_dn, int32_t dn_dtype, int8_t* ck,
+                      uint8_t* status, int32_t* iters, int32_t L, double alpha, double beta,
+                      int32_t schedule, int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok,
+                      uint32_t* tb_rem, uint8_t* tb_ok, void* stream);
+
 /* Message of the last failed call on this thread ("" if none). */
 const char* ldpc5g_last_error(void);
 

@@ -611,3 +611,62 @@ def raterecover(llr_fe, Ncb, N, k0, Qm, Zc, K_apo, K):
     out[:Ncb] = np.sum(tmp, axis=0) / cnt
     out[filler] = max_llr
     return out
+
+
+# -------------------------------------------------------------------- DL-SCH / UL-SCH chains
+def sch_params(A, Qm, R, NL, rv, TBS_LBRM, G):
+    """Shared geometry of DLSCHEncode / DLSCHDecode (nr_dlsch.py:30-66, nr_dlsch_decode.py:16-60);
+    TBS_LBRM = 0 selects the UL-SCH Ncb = N (nr_ulsch.py:55-58, nr_ulsch_decode.py:49-54)."""
+    B, poly = (A + 24, "24A") if A > 3824 else (A + 16, "16")
+    bgn = 2 if (A <= 292 or (A <= 3824 and R <= 0.67 * 1024) or R <= 0.25 * 1024) else 1
+    C, cbz, L, F, K, Zc = get_cbs_info(B, bgn)
+    N = (66 if bgn == 1 else 50) * Zc
+    Ncb = min(N, math.floor(TBS_LBRM / (C * 2 / 3))) if TBS_LBRM else N
+    return dict(A=A, B=B, poly=poly, bgn=bgn, C=C, cbz=cbz, L=L, F=F, K=K, Zc=Zc, N=N, Ncb=Ncb,
+                K_apo=cbz + L, k0=get_k0(Ncb, bgn, rv, Zc), Er=get_Er(G, C, Qm, NL), Qm=Qm)
+
+
+def sch_encode(trblk, A, Qm, R, NL, rv, TBS_LBRM, G):
+    """DLSCHEncode (nr_dlsch.py:12-74) / ULSCH encode (nr_ulsch.py:13-70) -> g (int8, G)."""
+    p = sch_params(A, Qm, R, NL, rv, TBS_LBRM, G)
+    cbs, _ = cbsegment(crc_encode(np.asarray(trblk), p["poly"]), p["bgn"])
+    g = np.zeros(G, np.int8)
+    off = 0
+    for c in range(p["C"]):
+        dn = encode(cbs[c], p["bgn"])
+        E = p["Er"][c]
+        g[off:off + E] = ratematch(dn, p["Ncb"], E, p["k0"], Qm)
+        off += E
+    return g
+
+
+def sch_raterecover(llr, p, harq=None):
+    """Per-codeblock rate recovery + HARQ combining (nr_dlsch_decode.py:62-88) -> (C, N)."""
+    llr = np.asarray(llr, np.float64)
+    out = np.zeros((p["C"], p["N"]))
+    off = 0
+    for c in range(p["C"]):
+        E = p["Er"][c]
+        d = raterecover(llr[off:off + E], p["Ncb"], p["N"], p["k0"], p["Qm"], p["Zc"],
+                        p["K_apo"], p["K"])
+        off += E
+        if harq is not None:
+            h = harq[c]
+            d = np.where((d == 0) | (h == 0), d + h, (d + h) / 2)
+        out[c] = d
+    return out
+
+
+def sch_tb_check(ck, p):
+    """TB reassembly + CRC checks (nr_dlsch_decode.py:93-106) of decoded (C, >=K_apo) bits ->
+    (tb_ok, tbblk int8[A], cb_crc_ok bool[C])."""
+    cbz, C = p["cbz"], p["C"]
+    tb = np.zeros(p["B"], np.int8)
+    cb_ok = np.ones(C, bool)
+    for c in range(C):
+        if C > 1:
+            _, err = crc_decode(ck[c, :p["K_apo"]], "24B")
+            cb_ok[c] = err == 0
+        tb[c * cbz:(c + 1) * cbz] = ck[c, :cbz]
+    blk, err = crc_decode(tb, p["poly"])
+    return err == 0, blk, cb_ok

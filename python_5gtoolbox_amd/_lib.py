@@ -37,6 +37,28 @@ SIGNATURES = {
     "ldpc5g_decode_bp": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                     _c.c_int64, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
                                     _c.c_int32, _c.c_int64, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_crc": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int32, _c.c_int32,
+                              _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_config": (_c.c_int, [_c.c_int32, _c.c_int32, _c.c_double, _c.c_int32, _c.c_int32,
+                                     _c.c_int64, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_sch_segment": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int32, _c.c_void_p,
+                                      _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_ratematch": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_void_p,
+                                        _c.c_void_p, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_sch_encode": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int64, _c.c_void_p,
+                                     _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                     _c.c_void_p]),
+    "ldpc5g_sch_raterecover": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p,
+                                          _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                          _c.c_void_p]),
+    "ldpc5g_sch_tb_check": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int32,
+                                       _c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_void_p,
+                                       _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_decode": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p, _c.c_int32,
+                                     _c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_void_p,
+                                     _c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_double,
+                                     _c.c_double, _c.c_int32, _c.c_void_p, _c.c_int64,
+                                     _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
     "ldpc5g_last_error": (_c.c_char_p, []),
     "ldpc5g_version": (_c.c_char_p, []),
 }
@@ -46,6 +68,20 @@ class CbDesc(ctypes.Structure):
     """ldpc5g_cb_desc_t"""
     _fields_ = [("bgn", ctypes.c_int32), ("Zc", ctypes.c_int32),
                 ("llr_off", ctypes.c_int64), ("ck_off", ctypes.c_int64)]
+
+
+CRC_IDS = {"6": 0, "11": 1, "16": 2, "24A": 3, "24B": 4, "24C": 5}
+
+
+class SchCfg(ctypes.Structure):
+    """ldpc5g_sch_cfg_t"""
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("A", "B", "tb_crc_poly", "bgn", "C", "cbz", "Lcb", "F", "K", "K_apo", "Zc", "N",
+                 "Ncb", "k0", "Qm", "NL", "rv", "E_lo", "E_hi", "c_switch")] + \
+               [("G", ctypes.c_int64), ("E_total", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 
 class LdpcLibError(RuntimeError):

@@ -26,6 +26,8 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+void clear_error() { g_err.clear(); }
+
 int zc_index(int Zc) {
     for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
         if (kLdpcZcList[i] == Zc) return i;

@@ -96,6 +96,7 @@ inline int dec_G(int Zc, bool layered = false) {
 
 // ---- host helpers (ldpc5g_capi.hip)
 int fail(int code, const char* fmt, ...);
+void clear_error();
 int zc_index(int Zc);
 int check_hip(hipError_t e, const char* what);
 

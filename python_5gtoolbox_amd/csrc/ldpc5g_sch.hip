@@ -1,0 +1,521 @@
+// ldpc5g_sch.hip — the DL-SCH / UL-SCH transport-channel chain around the LDPC codec, on the
+// GPU and batched over transport blocks that share one configuration (TS 38.212 §7.2 / §6.2):
+//   CRC attach / check ............ py5gphy/crc/crc.py:4-88
+//   codeblock segmentation ........ py5gphy/ldpc/nr_ldpc_cbsegment.py:7-33, ldpc_info.py:5-78
+//   rate matching ................. py5gphy/ldpc/nr_ldpc_ratematch.py:5-97
+//   rate recovery + HARQ combine .. py5gphy/ldpc/nr_ldpc_raterecover.py:6-65,
+//                                   py5gphy/nr_pdsch/nr_dlsch_decode.py:62-88
+//   TB reassembly + CRC checks .... py5gphy/nr_pdsch/nr_dlsch_decode.py:93-106
+// The chains themselves: DLSCHEncode (nr_dlsch.py:12-74), ULSCH_Crc_CodeBlockSegment +
+// ULSCH_encoding_ratematch (nr_ulsch.py:13-70), DLSCHDecode (nr_dlsch_decode.py:13-110),
+// ULSCH_decoding (nr_ulsch_decode.py:13-110).
+//
+// All of it is byte / integer work bound by HBM or latency, not arithmetic: bits stay one per
+// int8 (the reference's own representation and the encoder/decoder ABI), a wave packs 64 of them
+// with one ballot, and CRCs are combined across threads, codeblocks and transport blocks through
+// the linearity crc(M1 || M2) = crc(M1) * x^|M2| + crc(M2)  (mod g).
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "ldpc5g_common.h"
+
+namespace ldpc5g_impl {
+namespace {
+
+// ===================================================================================== CRC
+// Generators without the x^L term, coefficients x^(L-1) .. x^0 (crc.py:94-106).
+struct CrcPoly {
+    int L;
+    uint32_t g;
+};
+constexpr CrcPoly kCrcPoly[6] = {{6, 0x21u},      {11, 0x621u},     {16, 0x1021u},
+                                 {24, 0x864CFBu}, {24, 0x800063u}, {24, 0xB2B117u}};
+
+__host__ __device__ constexpr uint32_t crc_mulx(uint32_t a, int L, uint32_t g) {
+    return ((a << 1) & ((1u << L) - 1u)) ^ (((a >> (L - 1)) & 1u) ? g : 0u);
+}
+// a(x) * b(x) mod (x^L + g(x))
+__host__ __device__ constexpr uint32_t crc_mulmod(uint32_t a, uint32_t b, int L, uint32_t g) {
+    uint32_t r = 0;
+    for (int i = 0; i < L; ++i) {
+        if ((b >> i) & 1u) r ^= a;
+        a = crc_mulx(a, L, g);
+    }
+    return r;
+}
+
+constexpr int kCrcNT = 256;              // threads of a CRC workgroup
+constexpr int kCrcChunkWords = kCrcNT;   // 64-bit words per workgroup chunk (16384 bits)
+
+struct CrcTables {
+    uint32_t xp2[6][40];                // x^(2^i) mod g
+    uint32_t x64[6][kCrcChunkWords];    // x^(64 m) mod g
+};
+constexpr CrcTables make_crc_tables() {
+    CrcTables t{};
+    for (int p = 0; p < 6; ++p) {
+        const int L = kCrcPoly[p].L;
+        const uint32_t g = kCrcPoly[p].g;
+        t.xp2[p][0] = 2u;
+        for (int i = 1; i < 40; ++i) t.xp2[p][i] = crc_mulmod(t.xp2[p][i - 1], t.xp2[p][i - 1], L, g);
+        t.x64[p][0] = 1u;
+        for (int m = 1; m < kCrcChunkWords; ++m) t.x64[p][m] = crc_mulmod(t.x64[p][m - 1], t.xp2[p][6], L, g);
+    }
+    return t;
+}
+__constant__ CrcTables kCrcTab = make_crc_tables();
+
+__device__ uint32_t crc_xpow(int64_t n, int p) {   // x^n mod g
+    const int L = kCrcPoly[p].L;
+    const uint32_t g = kCrcPoly[p].g;
+    uint32_t r = 1u;
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) r = crc_mulmod(r, kCrcTab.xp2[p][i], L, g);
+    return r;
+}
+
+// CRC register of 64 message bits, bit 0 first: W(x) x^L mod g (crc.py:28-33 long division)
+__device__ __forceinline__ uint32_t crc_word64(uint64_t w, int L, uint32_t g) {
+    uint32_t reg = 0;
+    const uint32_t mask = (1u << L) - 1u;
+#pragma unroll
+    for (int b = 0; b < 64; ++b) {
+        const uint32_t fb = ((reg >> (L - 1)) ^ (uint32_t)(w >> b)) & 1u;
+        reg = ((reg << 1) & mask) ^ (fb ? g : 0u);
+    }
+    return reg;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Contribution of chunk `chunk` (64-bit words [256 chunk, 256 chunk + 256)) to the CRC of an
+// nbits-long message read through bitf(i) (0/1): crc(chunk) * x^(bits after the chunk).  The
+// message is left-padded with zeros to whole words (leading zeros do not change a CRC).  Valid
+// in thread 0; every thread of the (kCrcNT-thread) workgroup must call it.
+template <typename BitF>
+__device__ uint32_t wg_crc_chunk(BitF bitf, int64_t nbits, int64_t chunk, int p, uint32_t* red) {
+    const int L = kCrcPoly[p].L;
+    const uint32_t g = kCrcPoly[p].g;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nw = (nbits + 63) >> 6, pad = nw * 64 - nbits;
+    const int64_t q0 = chunk * kCrcChunkWords;
+    const int64_t qe = min(q0 + kCrcChunkWords - 1, nw - 1);   // last word of the chunk
+    uint64_t mine = 0;
+#pragma unroll 8
+    for (int k = 0; k < 64; ++k) {   // word q0 + 64 wv + k, bit `lane`: one coalesced 64-B row
+        const int64_t q = q0 + 64 * wv + k;
+        const int64_t i = q * 64 + lane - pad;
+        const bool b = q <= qe && i >= 0 && (bitf(i) & 1);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(b);
+        mine = lane == k ? m : mine;
+    }
+    const int64_t q = q0 + 64 * wv + lane;
+    uint32_t c = 0;
+    if (q <= qe) c = crc_mulmod(crc_word64(mine, L, g), kCrcTab.x64[p][qe - q], L, g);
+    c = wave_xor(c);
+    if (lane == 0) red[wv] = c;
+    __syncthreads();
+    uint32_t r = 0;
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < kCrcNT / 64; ++w) r ^= red[w];
+        r = crc_mulmod(r, crc_xpow(64 * (nw - 1 - qe), p), L, g);
+    }
+    __syncthreads();
+    return r;
+}
+
+__host__ __device__ inline int64_t crc_chunks(int64_t nbits) {
+    return ((nbits + 63) / 64 + kCrcChunkWords - 1) / kCrcChunkWords;
+}
+
+// rem[r] ^= crc contribution of chunk blockIdx.y of row r (rem zeroed by the launcher)
+__global__ __launch_bounds__(kCrcNT) void crc_rows_kernel(const int8_t* __restrict__ bits, int64_t ld,
+                                                          int64_t nbits, int p, uint32_t* rem) {
+    __shared__ uint32_t red[kCrcNT / 64];
+    const int8_t* row = bits + (int64_t)blockIdx.x * ld;
+    const uint32_t c = wg_crc_chunk([&](int64_t i) { return (int)row[i]; }, nbits, blockIdx.y, p, red);
+    if (threadIdx.x == 0 && c) atomicXor(&rem[blockIdx.x], c);
+}
+
+// ============================================================================ SCH geometry
+struct SchDev {
+    int32_t A, B, tbp, Ltb, bgn, C, cbz, Lcb, K, K_apo, Zc, N, Ncb, Qm;
+    int32_t E_lo, E_hi, c_switch;
+    int32_t f0, F, Fin, size, start;   // fillers [f0, f0+F) of dn; Fin of them below Ncb
+    int64_t G;
+};
+
+__device__ __forceinline__ int cb_E(const SchDev& s, int c) { return c < s.c_switch ? s.E_lo : s.E_hi; }
+__device__ __forceinline__ int64_t cb_goff(const SchDev& s, int c) {
+    return (int64_t)c * s.E_lo + (int64_t)max(0, c - s.c_switch) * (s.E_hi - s.E_lo);
+}
+// dn position of the k-th bit selected from the circular buffer (k0 first, fillers skipped)
+__device__ __forceinline__ int sel_pos(const SchDev& s, int64_t k) {
+    const int idx = (int)((s.start + k) % s.size);
+    return idx < s.f0 ? idx : idx + s.Fin;
+}
+
+// ------------------------------------------------------------------------------- transmit
+// TB CRC (24A / 16) of every transport block: tbcrc[t] ^= chunk contributions
+__global__ __launch_bounds__(kCrcNT) void tb_crc_kernel(const int8_t* __restrict__ trblk, int64_t lda,
+                                                        SchDev s, uint32_t* tbcrc) {
+    __shared__ uint32_t red[kCrcNT / 64];
+    const int8_t* row = trblk + (int64_t)blockIdx.x * lda;
+    const uint32_t c = wg_crc_chunk([&](int64_t i) { return (int)row[i]; }, s.A, blockIdx.y, s.tbp, red);
+    if (threadIdx.x == 0 && c) atomicXor(&tbcrc[blockIdx.x], c);
+}
+
+// codeblock segmentation + CRC24B (nr_ldpc_cbsegment.py:24-32): codeblock (t, c) -> ck row
+// t*C + c: cbz bits of (TB || TB CRC), its CRC24B when C > 1, fillers -1 up to K
+__global__ __launch_bounds__(kCrcNT) void cbseg_kernel(const int8_t* __restrict__ trblk, int64_t lda,
+                                                       const uint32_t* __restrict__ tbcrc, SchDev s,
+                                                       int8_t* __restrict__ ck) {
+    __shared__ uint32_t red[kCrcNT / 64];
+    __shared__ uint32_t cbcrc;
+    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const int8_t* tb = trblk + (int64_t)t * lda;
+    const uint32_t tc = tbcrc[t];
+    const int64_t base = (int64_t)c * s.cbz;
+    auto seg = [&](int64_t j) -> int {
+        const int64_t i = base + j;
+        return i < s.A ? (int)(tb[i] & 1) : (int)((tc >> (s.Ltb - 1 - (int)(i - s.A))) & 1u);
+    };
+    if (s.C > 1) {
+        const uint32_t v = wg_crc_chunk(seg, s.cbz, 0, LDPC5G_CRC24B, red);
+        if (threadIdx.x == 0) cbcrc = v;
+        __syncthreads();
+    }
+    int8_t* out = ck + (int64_t)r * s.K;
+    for (int j = threadIdx.x; j < s.K; j += kCrcNT) {
+        int8_t v = -1;
+        if (j < s.cbz) v = (int8_t)seg(j);
+        else if (j < s.K_apo) v = (int8_t)((cbcrc >> (23 - (j - s.cbz))) & 1u);
+        out[j] = v;
+    }
+}
+
+// rate matching (nr_ldpc_ratematch.py:64-97): bit selection from k0 skipping fillers, then the
+// Qm-row interleaver, written at the codeblock's offset in g (code block concatenation)
+__global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict__ dn, SchDev s,
+                                                        int8_t* __restrict__ g, int64_t ldg) {
+    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const int E = cb_E(s, c), EQ = E / s.Qm;
+    const int e = blockIdx.y * 256 + threadIdx.x;
+    if (e >= E) return;
+    const int q = e % s.Qm, i = e / s.Qm;
+    const int64_t k = (int64_t)q * EQ + i;
+    g[(int64_t)t * ldg + cb_goff(s, c) + e] = dn[(int64_t)r * s.N + sel_pos(s, k)];
+}
+
+// -------------------------------------------------------------------------------- receive
+constexpr int kRrNT = 512;
+
+template <typename Tin>
+__device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double)p[i]; }
+
+// rate recovery (nr_ldpc_raterecover.py:25-64) of codeblock (t, c) + HARQ combining
+// (nr_dlsch_decode.py:73-88).  Arithmetic in float64, as the reference: a position visited cnt
+// times holds (0.0 + v_0 + ... + v_{cnt-1}) / cnt (the row-by-row numpy sum of tmp_buf);
+// unvisited positions 0; fillers 10 * max|LLR| of the codeblock.  A float32 output is the
+// float64 result rounded once.
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restrict__ llr, int64_t ldg,
+                                                            SchDev s, const Tout* __restrict__ harq,
+                                                            Tout* __restrict__ out) {
+    __shared__ double red[kRrNT / 64];
+    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const int E = cb_E(s, c), EQ = E / s.Qm;
+    const Tin* fe = llr + (int64_t)t * ldg + cb_goff(s, c);
+    double m = 0.0;
+    for (int e = threadIdx.x; e < E; e += kRrNT) m = fmax(m, fabs(ld64(fe, e)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = red[0];
+#pragma unroll
+    for (int w = 1; w < kRrNT / 64; ++w) m = fmax(m, red[w]);
+    const double mx = m * 10.0;
+    const int64_t row = (int64_t)r * s.N;
+    for (int p = threadIdx.x; p < s.N; p += kRrNT) {
+        double v = 0.0;
+        if (p >= s.f0 && p < s.f0 + s.F) {
+            v = mx;
+        } else if (p < s.Ncb) {
+            int rr = (p < s.f0 ? p : p - s.Fin) - s.start;
+            if (rr < 0) rr += s.size;
+            if (rr < E) {
+                const int cnt = (E - 1 - rr) / s.size + 1;
+                double acc = 0.0;
+                for (int j = 0; j < cnt; ++j) {
+                    const int k = rr + j * s.size;
+                    acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
+                }
+                v = acc / (double)cnt;
+            }
+        }
+        if (harq) {
+            const double h = (double)harq[row + p];
+            v = (v == 0.0 || h == 0.0) ? v + h : (v + h) / 2.0;
+        }
+        out[row + p] = (Tout)v;
+    }
+}
+
+// TB reassembly + checks (nr_dlsch_decode.py:93-106) for codeblock (t, c): CB CRC24B over
+// ck[0:K_apo] when C > 1 (cb_ok = remainder 0), copy of ck[0:cbz] to the TB bits, and this
+// codeblock's share of the TB CRC remainder, crc(seg) * x^((C-1-c) cbz), XORed into tbrem[t].
+__global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restrict__ ck, int64_t ldc,
+                                                          SchDev s, int8_t* __restrict__ tbblk,
+                                                          int64_t ldb, uint8_t* __restrict__ cb_ok,
+                                                          uint32_t* tbrem) {
+    __shared__ uint32_t red[kCrcNT / 64];
+    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const int8_t* row = ck + (int64_t)r * ldc;
+    auto bit = [&](int64_t i) { return (int)row[i]; };
+    uint32_t cbr = 0;
+    if (s.C > 1) cbr = wg_crc_chunk(bit, s.K_apo, 0, LDPC5G_CRC24B, red);
+    uint32_t tbc = wg_crc_chunk(bit, s.cbz, 0, s.tbp, red);
+    int8_t* dst = tbblk + (int64_t)t * ldb + (int64_t)c * s.cbz;
+    for (int j = threadIdx.x; j < s.cbz; j += kCrcNT) dst[j] = row[j];
+    if (threadIdx.x == 0) {
+        cb_ok[r] = cbr == 0u;
+        tbc = crc_mulmod(tbc, crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp), s.Ltb, kCrcPoly[s.tbp].g);
+        if (tbc) atomicXor(&tbrem[t], tbc);
+    }
+}
+
+__global__ void tb_ok_kernel(const uint32_t* __restrict__ tbrem, uint8_t* __restrict__ ok, int T) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) ok[t] = tbrem[t] == 0u;
+}
+
+// ============================================================================ host helpers
+// cfg -> validated device geometry
+int sch_dev(const ldpc5g_sch_cfg_t* c, SchDev* s) {
+    if (!c) return fail(LDPC5G_ESIZE, "null cfg");
+    memset(s, 0, sizeof *s);
+    s->A = c->A, s->B = c->B, s->tbp = c->tb_crc_poly, s->bgn = c->bgn, s->C = c->C, s->cbz = c->cbz;
+    s->Lcb = c->Lcb, s->K = c->K, s->K_apo = c->K_apo, s->Zc = c->Zc, s->N = c->N, s->Ncb = c->Ncb;
+    s->Qm = c->Qm, s->E_lo = c->E_lo, s->E_hi = c->E_hi, s->c_switch = c->c_switch, s->G = c->G;
+    if (s->tbp != LDPC5G_CRC24A && s->tbp != LDPC5G_CRC16) return fail(LDPC5G_ESIZE, "cfg: bad TB CRC");
+    s->Ltb = kCrcPoly[s->tbp].L;
+    if (c->bgn != 1 && c->bgn != 2) return fail(LDPC5G_EBGN, "cfg: bgn=%d", c->bgn);
+    if (zc_index(c->Zc) < 0) return fail(LDPC5G_EZC, "cfg: Zc=%d", c->Zc);
+    if (c->K != (c->bgn == 1 ? 22 : 10) * c->Zc || c->N != (c->bgn == 1 ? 66 : 50) * c->Zc)
+        return fail(LDPC5G_ESIZE, "cfg: K/N inconsistent with (bgn, Zc)");
+    if (c->C < 1 || (int64_t)c->cbz * c->C != c->B || c->K_apo != c->cbz + c->Lcb || c->K_apo > c->K ||
+        (c->C > 1) != (c->Lcb == 24) || c->Ncb < 1 || c->Ncb > c->N || c->A < 1 || c->B <= c->A)
+        return fail(LDPC5G_ESIZE, "cfg: inconsistent segmentation");
+    if (c->Qm < 1 || c->E_lo < 0 || c->E_hi < c->E_lo || c->E_lo % c->Qm || c->E_hi % c->Qm ||
+        c->c_switch < 0 || c->c_switch > c->C || c->k0 < 0 || c->k0 >= c->Ncb)
+        return fail(LDPC5G_ESIZE, "cfg: inconsistent rate matching");
+    s->f0 = c->K_apo - 2 * c->Zc;
+    s->F = c->K - c->K_apo;
+    if (s->f0 < 0) return fail(LDPC5G_ESIZE, "cfg: fillers before 2Zc");
+    s->Fin = s->f0 < c->Ncb ? std::min(s->f0 + s->F, c->Ncb) - s->f0 : 0;
+    s->size = c->Ncb - s->Fin;
+    if (s->size < 1) return fail(LDPC5G_ESIZE, "cfg: empty circular buffer");
+    const int k0 = c->k0;
+    s->start = k0 < s->f0 ? k0 : (k0 < s->f0 + s->Fin ? s->f0 : k0 - s->Fin);
+    return LDPC5G_OK;
+}
+
+int64_t sch_total_E(const SchDev& s) {
+    return (int64_t)s.c_switch * s.E_lo + (int64_t)(s.C - s.c_switch) * s.E_hi;
+}
+
+}  // namespace
+}  // namespace ldpc5g_impl
+
+using namespace ldpc5g_impl;
+
+extern "C" {
+
+int ldpc5g_crc(const int8_t* bits, int64_t ld, int64_t nbits, int32_t rows, int32_t poly,
+               uint32_t* rem, void* stream) {
+    clear_error();
+    if (poly < 0 || poly > 5) return fail(LDPC5G_ESIZE, "bad CRC polynomial id %d", poly);
+    if (rows < 0 || nbits < 0 || (rows > 1 && ld < nbits)) return fail(LDPC5G_ESIZE, "bad sizes");
+    if (rows == 0) return LDPC5G_OK;
+    if (!rem || (nbits > 0 && !bits)) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = check_hip(hipMemsetAsync(rem, 0, (size_t)rows * 4, st), "hipMemsetAsync")) return rc;
+    if (nbits == 0) return LDPC5G_OK;
+    hipLaunchKernelGGL(crc_rows_kernel, dim3(rows, (unsigned)crc_chunks(nbits)), dim3(kCrcNT), 0, st,
+                       bits, ld, nbits, (int)poly, rem);
+    return check_hip(hipGetLastError(), "crc_rows_kernel launch");
+}
+
+int ldpc5g_sch_config(int32_t A, int32_t Qm, double coderateby1024, int32_t NL, int32_t rv,
+                      int64_t TBS_LBRM, int64_t G, ldpc5g_sch_cfg_t* c) {
+    clear_error();
+    if (!c) return fail(LDPC5G_ESIZE, "null cfg");
+    memset(c, 0, sizeof *c);
+    if (A < 1 || Qm < 1 || Qm > 10 || NL < 1 || G < 1 || TBS_LBRM < 0)
+        return fail(LDPC5G_ESIZE, "bad SCH parameters A=%d Qm=%d NL=%d G=%lld", A, Qm, NL, (long long)G);
+    if (rv < 0 || rv > 3) return fail(LDPC5G_ESIZE, "rv=%d not in [0,3] (nr_ldpc_ratematch.py:46)", rv);
+    // TB CRC (nr_dlsch.py:34-40) and base graph selection (:44-49)
+    c->A = A;
+    c->B = A > 3824 ? A + 24 : A + 16;
+    c->tb_crc_poly = A > 3824 ? LDPC5G_CRC24A : LDPC5G_CRC16;
+    const double R = coderateby1024;
+    c->bgn = (A <= 292 || (A <= 3824 && R <= 0.67 * 1024) || R <= 0.25 * 1024) ? 2 : 1;
+    // get_cbs_info (ldpc_info.py:5-78)
+    const int B = c->B, Kcb = c->bgn == 1 ? 8448 : 3840;
+    int C, L, Bd;
+    if (B <= Kcb) {
+        L = 0, C = 1, Bd = B;
+    } else {
+        L = 24;
+        C = (int)ceil((double)B / (double)(Kcb - L));
+        Bd = B + C * L;
+    }
+    if (B % C || Bd % C) return fail(LDPC5G_ESIZE, "B=%d does not split into %d codeblocks", B, C);
+    const int cbz = B / C, Kd = Bd / C;
+    int Kb = 22;
+    if (c->bgn == 2) Kb = B > 640 ? 10 : B > 560 ? 9 : B > 192 ? 8 : 6;
+    int Zc = -1;
+    for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi)   // ascending
+        if (kLdpcZcList[zi] * Kb >= Kd) {
+            Zc = kLdpcZcList[zi];
+            break;
+        }
+    if (Zc < 0) return fail(LDPC5G_ESIZE, "no lifting size for K'=%d", Kd);
+    c->C = C, c->cbz = cbz, c->Lcb = L, c->Zc = Zc;
+    c->K = (c->bgn == 1 ? 22 : 10) * Zc;
+    c->F = c->K - Kd;
+    c->K_apo = cbz + L;
+    c->N = (c->bgn == 1 ? 66 : 50) * Zc;
+    // Ncb (nr_dlsch.py:63-65: I_LBRM = 1 with TBS_LBRM; nr_ulsch.py:55-58: Ncb = N when 0)
+    int64_t Ncb = c->N;
+    if (TBS_LBRM > 0) {
+        const double nref = floor((double)TBS_LBRM / ((double)(C * 2) / 3.0));
+        if (nref < Ncb) Ncb = (int64_t)nref;
+    }
+    c->Ncb = (int32_t)Ncb;
+    // k0 (nr_ldpc_ratematch.py:29-61)
+    static const int num1[4] = {0, 17, 33, 56}, num2[4] = {0, 13, 25, 43};
+    const int num = c->bgn == 1 ? num1[rv] : num2[rv], den = c->bgn == 1 ? 66 : 50;
+    c->k0 = (int32_t)floor((double)((int64_t)num * Ncb) / (double)(den * Zc)) * Zc;
+    c->Qm = Qm, c->NL = NL, c->rv = rv, c->G = G;
+    // Er (nr_ldpc_ratematch.py:5-27), float arithmetic as the reference
+    const double gq = (double)G / (double)(NL * Qm);
+    c->E_lo = NL * Qm * (int32_t)floor((double)G / (double)(NL * Qm * C));
+    c->E_hi = NL * Qm * (int32_t)ceil((double)G / (double)(NL * Qm * C));
+    const double thr = (double)C - fmod(gq, (double)C) - 1.0;
+    int cs = 0;
+    for (int j = 0; j < C; ++j) cs += (double)j <= thr;
+    c->c_switch = cs;
+    SchDev s;
+    if (int rc = sch_dev(c, &s)) return rc;
+    c->E_total = sch_total_E(s);
+    return LDPC5G_OK;
+}
+
+int ldpc5g_sch_segment(const int8_t* trblk, int64_t lda, const ldpc5g_sch_cfg_t* cfg, int32_t T,
+                       int8_t* ck, uint32_t* tb_crc, void* stream) {
+    clear_error();
+    SchDev s;
+    if (int rc = sch_dev(cfg, &s)) return rc;
+    if (T < 0 || (T > 1 && lda < s.A)) return fail(LDPC5G_ESIZE, "bad sizes T=%d lda=%lld", T, (long long)lda);
+    if (T == 0) return LDPC5G_OK;
+    if (!trblk || !ck || !tb_crc) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = check_hip(hipMemsetAsync(tb_crc, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
+    hipLaunchKernelGGL(tb_crc_kernel, dim3(T, (unsigned)crc_chunks(s.A)), dim3(kCrcNT), 0, st, trblk,
+                       lda, s, tb_crc);
+    hipLaunchKernelGGL(cbseg_kernel, dim3(T * s.C), dim3(kCrcNT), 0, st, trblk, lda,
+                       (const uint32_t*)tb_crc, s, ck);
+    return check_hip(hipGetLastError(), "segment launch");
+}
+
+int ldpc5g_sch_ratematch(const int8_t* ck, const ldpc5g_sch_cfg_t* cfg, int32_t T, int8_t* dn,
+                         int8_t* g, int64_t ldg, void* stream) {
+    clear_error();
+    SchDev s;
+    if (int rc = sch_dev(cfg, &s)) return rc;
+    if (T < 0 || (T > 1 && ldg < sch_total_E(s))) return fail(LDPC5G_ESIZE, "bad sizes T=%d ldg=%lld", T, (long long)ldg);
+    if (T == 0) return LDPC5G_OK;
+    if (!ck || !dn || !g) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const int rows = T * s.C;
+    if (int rc = launch_encode(ck, dn, rows, s.bgn, s.Zc, zc_index(s.Zc), s.K, s.N, st)) return rc;
+    if (s.E_hi > 0)
+        hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (s.E_hi + 255) / 256), dim3(256), 0, st, dn, s,
+                           g, ldg);
+    return check_hip(hipGetLastError(), "ratematch launch");
+}
+
+int ldpc5g_sch_encode(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
+                      const ldpc5g_sch_cfg_t* cfg, int32_t T, int8_t* ck, int8_t* dn,
+                      uint32_t* tb_crc, void* stream) {
+    if (int rc = ldpc5g_sch_segment(trblk, lda, cfg, T, ck, tb_crc, stream)) return rc;
+    return ldpc5g_sch_ratematch(ck, cfg, T, dn, g, ldg, stream);
+}
+
+int ldpc5g_sch_raterecover(const void* llr, int32_t llr_dtype, int64_t ldg,
+                           const ldpc5g_sch_cfg_t* cfg, int32_t T, const void* harq_in,
+                           void* llr_dn, int32_t dn_dtype, void* stream) {
+    clear_error();
+    SchDev s;
+    if (int rc = sch_dev(cfg, &s)) return rc;
+    if ((llr_dtype != LDPC5G_F32 && llr_dtype != LDPC5G_F64) || (dn_dtype != LDPC5G_F32 && dn_dtype != LDPC5G_F64))
+        return fail(LDPC5G_ESIZE, "bad dtype");
+    if (T < 0 || (T > 1 && ldg < sch_total_E(s))) return fail(LDPC5G_ESIZE, "bad sizes T=%d ldg=%lld", T, (long long)ldg);
+    if (T == 0) return LDPC5G_OK;
+    if (!llr || !llr_dn) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(T * s.C), blk(kRrNT);
+    if (llr_dtype == LDPC5G_F32 && dn_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<float, float>), grid, blk, 0, st, (const float*)llr, ldg, s, (const float*)harq_in, (float*)llr_dn);
+    else if (llr_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<float, double>), grid, blk, 0, st, (const float*)llr, ldg, s, (const double*)harq_in, (double*)llr_dn);
+    else if (dn_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<double, float>), grid, blk, 0, st, (const double*)llr, ldg, s, (const float*)harq_in, (float*)llr_dn);
+    else
+        hipLaunchKernelGGL((raterecover_kernel<double, double>), grid, blk, 0, st, (const double*)llr, ldg, s, (const double*)harq_in, (double*)llr_dn);
+    return check_hip(hipGetLastError(), "raterecover launch");
+}
+
+int ldpc5g_sch_tb_check(const int8_t* ck, int64_t ldc, const ldpc5g_sch_cfg_t* cfg, int32_t T,
+                        int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok, uint32_t* tb_rem,
+                        uint8_t* tb_ok, void* stream) {
+    clear_error();
+    SchDev s;
+    if (int rc = sch_dev(cfg, &s)) return rc;
+    if (T < 0 || ldc < s.K_apo || (T > 1 && ldb < s.B))
+        return fail(LDPC5G_ESIZE, "bad sizes T=%d ldc=%lld ldb=%lld", T, (long long)ldc, (long long)ldb);
+    if (T == 0) return LDPC5G_OK;
+    if (!ck || !tbblk || !cb_crc_ok || !tb_rem || !tb_ok) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = check_hip(hipMemsetAsync(tb_rem, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
+    hipLaunchKernelGGL(tb_check_kernel, dim3(T * s.C), dim3(kCrcNT), 0, st, ck, ldc, s, tbblk, ldb,
+                       cb_crc_ok, tb_rem);
+    hipLaunchKernelGGL(tb_ok_kernel, dim3((T + 255) / 256), dim3(256), 0, st, (const uint32_t*)tb_rem,
+                       tb_ok, (int)T);
+    return check_hip(hipGetLastError(), "tb_check launch");
+}
+
+int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldpc5g_sch_cfg_t* cfg,
+                      int32_t T, const void* harq_in, void* llr_dn, int32_t dn_dtype, int8_t* ck,
+                      uint8_t* status, int32_t* iters, int32_t L, double alpha, double beta,
+                      int32_t schedule, int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok,
+                      uint32_t* tb_rem, uint8_t* tb_ok, void* stream) {
+    if (int rc = ldpc5g_sch_raterecover(llr, llr_dtype, ldg, cfg, T, harq_in, llr_dn, dn_dtype, stream)) return rc;
+    if (T == 0) return LDPC5G_OK;
+    const int Nf = (cfg->bgn == 1 ? 68 : 52) * cfg->Zc;
+    if (int rc = ldpc5g_decode_ms(llr_dn, dn_dtype, ck, status, iters, T * cfg->C, cfg->bgn, cfg->Zc, L,
+                                  alpha, beta, schedule, 0, cfg->N, Nf, stream))
+        return rc;
+    return ldpc5g_sch_tb_check(ck, Nf, cfg, T, tbblk, ldb, cb_crc_ok, tb_rem, tb_ok, stream);
+}
+
+}  // extern "C"

@@ -15,6 +15,7 @@ the float64 widening of those float32 values so the fixtures are exact for both 
   ratematch_golden.npz ratematch_ldpc / raterecover_ldpc / get_k0 / get_Er cases
   crc_golden.json      CRC KATs (the inline vectors of py5gphy/crc/crc.py:167-210) + generated
   dlsch_golden.npz     DLSCHEncode (nr_dlsch.py:12) transport blocks -> g_seq
+  sch_golden.npz/.json DLSCHDecode (+HARQ), ULSCH encode/decode, a config-5 DLSCHEncode TB
   decode_bf_golden.npz / decode_bp_golden.npz   nr_decode_ldpc with algo='BF' / 'BP'
 """
 import json
@@ -319,10 +320,78 @@ def gen_dlsch():
     print("dlsch cases", len(rows))
 
 
+# ------------------------------------------------------------------ SCH chain (TX + RX, DL + UL)
+def _sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, np.float64).tobytes()).hexdigest()
+
+
+def gen_sch():
+    """DLSCHDecode / ULSCH_decoding (+ HARQ) and UL-SCH encode, and one full-size config-5
+    transport block through DLSCHEncode.  LLRs are stored float32 and the reference runs on
+    their float64 widening; new_LLr_dns is pinned by a sha256 of its float64 bytes."""
+    from py5gphy.nr_pdsch import nr_dlsch, nr_dlsch_decode
+    from py5gphy.nr_pusch import nr_ulsch, nr_ulsch_decode
+    rng = np.random.default_rng(21)
+    cases, blobs = [], {}
+    dec_cfg = {"L": 6, "algo": "min-sum", "alpha": 0.8, "beta": 0.0}
+    # (kind, TBS, Qm, R*1024, NL, rv, LBRM, G, snr_db)
+    specs = [("dl", 12000, 4, 517, 1, 0, 30000, 25000, 3.0),
+             ("dl", 12000, 4, 517, 1, 0, 30000, 25000, -1.0),
+             ("dl", 1800, 2, 308, 1, 0, 40000, 6000, 1.0),
+             ("ul", 8000, 2, 600, 1, 0, 0, 16000, 2.0),
+             ("ul", 2000, 4, 200, 1, 3, 0, 9000, 0.0)]
+    for n, (kind, TBS, Qm, R, NL, rv, LBRM, G, snr) in enumerate(specs):
+        trblk = rng.integers(0, 2, TBS)
+        if kind == "dl":
+            g = nr_dlsch.DLSCHEncode(trblk, TBS, Qm, R, NL, rv, LBRM, G)
+        else:
+            cbs, Zc, bgn = nr_ulsch.ULSCH_Crc_CodeBlockSegment(trblk, TBS, R)
+            blobs[f"cbs{n}"] = np.packbits((cbs.reshape(-1) == 1).astype(np.uint8))
+            blobs[f"cbsfill{n}"] = np.array([cbs.shape[0], cbs.shape[1], int(np.sum(cbs[0] == -1))])
+            g = nr_ulsch.ULSCH_encoding_ratematch(cbs, Zc, bgn, Qm, G, NL, rv)
+        llr = bpsk_llr(g, snr, rng).astype(np.float32)
+        x = llr.astype(np.float64)
+        if kind == "dl":
+            ok, tbblk, new = nr_dlsch_decode.DLSCHDecode(x, TBS, Qm, R, NL, rv, LBRM, dec_cfg)
+            # HARQ retransmission (rv 2) combined with the first decoder input
+            g2 = nr_dlsch.DLSCHEncode(trblk, TBS, Qm, R, NL, 2, LBRM, G)
+            llr2 = bpsk_llr(g2, snr, rng).astype(np.float32)
+            ok2, tb2, new2 = nr_dlsch_decode.DLSCHDecode(llr2.astype(np.float64), TBS, Qm, R, NL, 2,
+                                                         LBRM, dec_cfg, True, new)
+        else:
+            ok, tbblk, new = nr_ulsch_decode.ULSCH_decoding(x, TBS, R, Qm, G, NL, rv, dec_cfg)
+            llr2, ok2, tb2, new2 = np.zeros(1, np.float32), ok, tbblk, new
+        cases.append({"kind": kind, "TBS": TBS, "Qm": Qm, "R": R, "NL": NL, "rv": rv,
+                      "LBRM": LBRM, "G": G, "snr": snr, "ok": bool(ok), "ok2": bool(ok2),
+                      "new_sha": _sha(new), "new2_sha": _sha(new2), "new_shape": list(new.shape),
+                      "new_sum": float(np.sum(new))})
+        blobs[f"trblk{n}"] = np.packbits(trblk.astype(np.uint8))
+        blobs[f"g{n}"] = np.packbits((g == 1).astype(np.uint8))
+        blobs[f"llr{n}"] = llr
+        blobs[f"llr2_{n}"] = llr2
+        blobs[f"tbblk{n}"] = np.packbits(np.asarray(tbblk).astype(np.uint8))
+        blobs[f"tbblk2_{n}"] = np.packbits(np.asarray(tb2).astype(np.uint8))
+        print("sch case", n, kind, "ok", ok, "ok2", ok2, flush=True)
+    # config 5: 273 PRB 256QAM 4 layers, TBS 1,081,512 (dl_tbsize.py:308-317), C = 129
+    TBS, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
+    trblk = rng.integers(0, 2, TBS)
+    g = nr_dlsch.DLSCHEncode(trblk, TBS, Qm, R, NL, rv, TBS, G)
+    cases.append({"kind": "dl-encode", "TBS": TBS, "Qm": Qm, "R": R, "NL": NL, "rv": rv,
+                  "LBRM": TBS, "G": G})
+    n = len(cases) - 1
+    blobs[f"trblk{n}"] = np.packbits(trblk.astype(np.uint8))
+    blobs[f"g{n}"] = np.packbits((g == 1).astype(np.uint8))
+    np.savez_compressed(os.path.join(OUT, "sch_golden.npz"), **blobs)
+    with open(os.path.join(OUT, "sch_golden.json"), "w") as f:
+        json.dump(cases, f, indent=0)
+    print("sch cases", len(cases))
+
+
 if __name__ == "__main__":
     os.chdir(REF)
     sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
-    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "decode", "bfbp"]
+    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "decode", "bfbp"]
     if "encode" in which:
         gen_encode()
     if "crc" in which:
@@ -331,6 +400,8 @@ if __name__ == "__main__":
         gen_ratematch()
     if "dlsch" in which:
         gen_dlsch()
+    if "sch" in which:
+        gen_sch()
     if "decode" in which:
         with mp.get_context("fork").Pool(6) as pool:
             gen_decode(pool)
