@@ -114,6 +114,89 @@ def cpu_baseline(seconds, schedule, alpha, L):
                         "(BASELINE.md §2); the reference cannot travel to the GPU box"}}
 
 
+def bench_config4(torch, dist, world, dev, rank, steps):
+    """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
+    (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
+    GPU chain (encode -> rate match -> BPSK+AWGN -> rate recover), OMS beta=0.5, L=8, decoded by
+    ldpc5g_decode_ms_mixed (one call, two launches: BG1 / BG2 work lists)."""
+    import numpy as np
+    from python_5gtoolbox_amd.ldpc_info import code_dims
+    from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
+    from python_5gtoolbox_amd.sch import cfg_from_codeblocks, sch_ratematch_batch, \
+        sch_raterecover_batch
+    rng = np.random.default_rng(404 + rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(404 + rank)
+    n_per, snr = 341, 1.0
+    groups, info_bits = [], 0
+    for Zc in (12, 40, 72, 176, 208, 384):
+        for bg in (1, 2):
+            K, N, _ = code_dims(bg, Zc)
+            Qm = int(rng.choice([2, 4, 6, 8]))
+            rv = int(rng.integers(0, 4))
+            E = Qm * int(rng.integers(-(-K // Qm), int(1.6 * N) // Qm + 1))
+            cfg = cfg_from_codeblocks(n_per, K, K, Zc, bg, Qm, n_per * E, 1, rv)
+            ck = torch.randint(0, 2, (n_per, K), dtype=torch.int8, device=dev, generator=g)
+            gs = sch_ratematch_batch(ck, cfg, 1)
+            sigma = 10 ** (-snr / 20)
+            y = (1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g)
+            llr = (2 * y / sigma ** 2).contiguous()
+            dn = sch_raterecover_batch(llr, cfg, dn_dtype=torch.float32).clone()
+            groups.append((bg, Zc, dn))
+            info_bits += n_per * K
+    mb = MixedBatch(groups)
+    B = mb.B
+    wall, _ = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered"), steps, 2)
+    _, st, it = mb.decode(8, 1.0, 0.5, "layered")
+    return {"workload": "BASELINE config 4: 12 (Zc, BG) groups x 341 CBs, random (Qm, rv, E), "
+                        "GPU rate match/recover, snr 1 dB, layered OMS beta=0.5 L=8",
+            "codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
+            "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
+            "ms_per_call": round(wall / steps * 1e3, 4),
+            "mean_iterations": round(it.float().mean().item(), 3),
+            "converged_frac": round(st.float().mean().item(), 4)}
+
+
+def bench_config5(torch, dist, world, dev, rank, steps, T=32):
+    """BASELINE config 5: PDSCH 273 PRB 256QAM MCS27 4 layers TB stream (TBS 1,081,512 ->
+    129 BG1 Zc=384 codeblocks per TB, G = 8*4*36036), T TBs per GPU: the GPU DL-SCH chain both
+    ways (ldpc5g_sch_encode; ldpc5g_sch_decode = rate recovery + layered NMS L=8 + CB/TB CRCs),
+    LLRs from BPSK + AWGN on the rate-matched bits (no modem: the chain's input is LLRs)."""
+    from python_5gtoolbox_amd.sch import SchWorkspace, sch_config, sch_decode_batch, \
+        sch_encode_batch
+    A, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
+    cfg = sch_config(A, Qm, R, NL, rv, A, G)
+    g = torch.Generator(device=dev)
+    g.manual_seed(505 + rank)
+    tb = torch.randint(0, 2, (T, A), dtype=torch.int8, device=dev, generator=g)
+    ws = SchWorkspace(cfg, T, dev)
+    wt, _ = timed(torch, dist, world, lambda: sch_encode_batch(tb, cfg, ws), steps, 2)
+    gs = sch_encode_batch(tb, cfg, ws)
+    snr = 6.0
+    sigma = 10 ** (-snr / 20)
+    llr = (2 * ((1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g))
+           / sigma ** 2).contiguous()
+
+    def rx():
+        sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+    wr, _ = timed(torch, dist, world, rx, steps, 2)
+    r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+    ok = bool(torch.equal(r.tbblk[:, :A], tb))
+    return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, BG1 Zc=384, "
+                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), snr {snr} dB BPSK-AWGN LLRs",
+            "tb_per_gpu": T, "codeblocks_per_tb": cfg.C,
+            "rx_tb_per_s": round(T * world * steps / wr, 2),
+            "rx_codeblocks_per_s": round(T * cfg.C * world * steps / wr, 1),
+            "rx_info_gbit_s": round(T * A * world * steps / wr / 1e9, 3),
+            "rx_ms_per_batch": round(wr / steps * 1e3, 4),
+            "tx_tb_per_s": round(T * world * steps / wt, 2),
+            "tx_info_gbit_s": round(T * A * world * steps / wt / 1e9, 3),
+            "tx_ms_per_batch": round(wt / steps * 1e3, 4),
+            "tb_crc_ok_frac": round(r.tb_ok.float().mean().item(), 4),
+            "tb_bits_match": ok,
+            "mean_iterations": round(r.iters.float().mean().item(), 3)}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -215,6 +298,8 @@ def main():
                                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                              "frac": round(ach / HBM_PEAK_GBS, 4),
                                              "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB}}
+        ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2))
+        ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
         res["extras"] = ex
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

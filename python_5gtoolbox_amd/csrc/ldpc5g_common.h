@@ -74,6 +74,15 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also releases global memory at
+// workgroup scope, i.e. waits (vmcnt(0)) for every outstanding global load AND store of the wave;
+// kernels that exchange data only through LDS use this one so stores and prefetches stay in flight.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 struct DecWork {     // one workgroup of the mixed-Zc path
     int32_t zi, Zc, G, first;
 };

@@ -2,6 +2,9 @@
 // Part of libldpc5g.so (MI355X, gfx950); reference mapping in ldpc5g_common.h / DESIGN.md §4.
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "ldpc5g_common.h"
 
@@ -291,75 +294,54 @@ __device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits
     }
 }
 
-template <int BG>
-__global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
-                                                            int8_t* __restrict__ dn, int B, int Zc,
-                                                            int zi, int64_t ldk, int64_t ldn) {
+// Phase 1 of the fast encoder for one 32-byte chunk (word wi): pack the parity bits (fillers at
+// k >= 2Zc -> 0, nr_ldpc_encode.py:32-37) and store the systematic bytes straight to dn.
+__device__ __forceinline__ uint32_t enc_pack_chunk(const int4 (&v)[2], int base, int twoZ, int8_t* dst) {
+    if (base >= twoZ) {   // 2Zc and K are multiples of 32 here
+        *(int4*)(dst + base - twoZ) = v[0];
+        *(int4*)(dst + base - twoZ + 16) = v[1];
+    }
+    const uint32_t* d = (const uint32_t*)v;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t x = d[q];
+        // per byte: LSB, minus fillers (0xff) at positions >= 2Zc
+        uint32_t lsb = x & 0x01010101u;
+        const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                             (x >> 6) & (x >> 7)) & 0x01010101u;   // byte == 0xff
+        if (base + 4 * q >= twoZ) lsb &= ~ff;
+        bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+    }
+    return bits;
+}
+
+template <bool LDSONLY>
+__device__ __forceinline__ void enc_sync() {
+    if constexpr (LDSONLY) lds_sync();
+    else __syncthreads();
+}
+
+// Phases 2-6 of the fast encoder for one codeblock whose packed bits are in ib (LDS): parity
+// straight to dst.  LDSONLY: barriers order LDS only, so the systematic stores, parity stores and
+// (pipelined kernel) the next codeblock's loads stay in flight across them.
+template <int BG, bool LDSONLY>
+__device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_t* sm, int8_t* dst,
+                                                int Zc, int zi, int t, int NT) {
     using P = BGT<BG>;
-    const int b = blockIdx.x;
-    if (b >= B) return;
-    const int t = threadIdx.x;
-    const int NT = blockDim.x;
-    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
     const int K = Ly.K, W = Ly.W, DW = Ly.DW, KW = Ly.KW;
-    const int twoZ = 2 * Zc;
-    const int S = K - twoZ;
-    extern __shared__ __align__(16) uint32_t sm[];
+    const int S = K - 2 * Zc;
     uint32_t* ib = sm;
     uint32_t* X = ib + KW + 2;
     uint32_t* lam = X + P::KC * DW;
     uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
-    const int8_t* src = ck + (int64_t)b * ldk;
-    int8_t* dst = dn + (int64_t)b * ldn;
-
-    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn
-    for (int wi = t; wi < KW; wi += NT) {
-        const int base = wi * 32;   // K = Kb*Zc is a multiple of 32 when Zc % 16 == 0
-        uint32_t bits = 0;
-        if (base + 32 <= K) {
-            int4 v[2];
-            v[0] = *(const int4*)(src + base);
-            v[1] = *(const int4*)(src + base + 16);
-            if (base >= twoZ) {   // 2Zc and K are multiples of 32 here
-                *(int4*)(dst + base - twoZ) = v[0];
-                *(int4*)(dst + base - twoZ + 16) = v[1];
-            }
-            const uint32_t* d = (const uint32_t*)v;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t x = d[q];
-                // per byte: LSB, minus fillers (0xff) at positions >= 2Zc
-                uint32_t lsb = x & 0x01010101u;
-                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
-                                     (x >> 6) & (x >> 7)) & 0x01010101u;   // byte == 0xff
-                if (base + 4 * q >= twoZ) lsb &= ~ff;
-                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
-            }
-        } else {   // (unreachable for Kb*Zc % 32 == 0; kept for safety)
-            int4 v0 = *(const int4*)(src + base);
-            if (base >= twoZ) *(int4*)(dst + base - twoZ) = v0;
-            const uint32_t* d = (const uint32_t*)&v0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t x = d[q];
-                uint32_t lsb = x & 0x01010101u;
-                const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
-                                     (x >> 6) & (x >> 7)) & 0x01010101u;
-                if (base + 4 * q >= twoZ) lsb &= ~ff;
-                bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
-            }
-        }
-        ib[wi] = bits;
-    }
-    if (t < 2) ib[KW + t] = 0;
-    __syncthreads();
 
     // ---- 2. periodic extensions of the information columns
     for (int task = t; task < P::KB * DW; task += NT) {
         int j = task / DW, q = task - j * DW;
         X[j * DW + q] = fetch_rot32(ib, j * Zc, Zc, mod_zc(32 * q, Zc));
     }
-    __syncthreads();
+    enc_sync<LDSONLY>();
 
     // ---- 3+4. lambda and the double-diagonal recursion, all inside wave 0
     constexpr int eS = (BG == 1) ? edge_of<BG>(1, 22) : edge_of<BG>(2, 10);
@@ -402,7 +384,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
             else p3[w] = lam[1 * W + w] ^ fetch_rot32(p2, 0, Zc, mod_zc(32 * w + shift_of<BG>(zi, eD), Zc));
         }
     }
-    __syncthreads();
+    enc_sync<LDSONLY>();
 
     // ---- 5. extensions of the 4 core parity columns; core parity bytes straight to dn
     for (int task = t; task < 4 * DW; task += NT) {
@@ -413,7 +395,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
         int k = task / W, w = task - k * W;
         store_bits(dst + S + k * Zc + 32 * w, pv[k * W + w], min(32, Zc - 32 * w));
     }
-    __syncthreads();
+    enc_sync<LDSONLY>();
 
     // ---- 6. extension parity rows, each row-word stored straight to dn
     for (int task = t; task < (P::MB - 4) * W; task += NT) {
@@ -427,6 +409,75 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     }
 }
 
+template <int BG, bool LDSONLY>
+__global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
+                                                            int8_t* __restrict__ dn, int B, int Zc,
+                                                            int zi, int64_t ldk, int64_t ldn) {
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int t = threadIdx.x;
+    const int NT = blockDim.x;
+    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
+    const int twoZ = 2 * Zc;
+    extern __shared__ __align__(16) uint32_t sm[];
+    const int8_t* src = ck + (int64_t)b * ldk;
+    int8_t* dst = dn + (int64_t)b * ldn;
+    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn
+    for (int wi = t; wi < Ly.KW; wi += NT) {   // K = Kb*Zc is a multiple of 32 when Zc % 16 == 0
+        int4 v[2];
+        v[0] = *(const int4*)(src + wi * 32);
+        v[1] = *(const int4*)(src + wi * 32 + 16);
+        sm[wi] = enc_pack_chunk(v, wi * 32, twoZ, dst);
+    }
+    if (t < 2) sm[Ly.KW + t] = 0;
+    enc_sync<LDSONLY>();
+    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT);
+}
+
+// Pipelined persistent encoder: a workgroup encodes codeblocks b, b + grid, b + 2 grid, ...; the
+// next codeblock's information bytes are loaded into registers while the current one's parity
+// is computed and stored, so HBM reads, LDS work and HBM writes of consecutive codeblocks overlap
+// (the one-codeblock-per-workgroup kernel runs every CU's codeblocks through the same phase at
+// the same time).  256 threads, <= 2 chunks of 32 B per thread (K <= 8448).
+constexpr int kEncPipeNT = 256;
+template <int BG>
+__global__ __launch_bounds__(kEncPipeNT) void ldpc_enc_pipe_kernel(const int8_t* __restrict__ ck,
+                                                                   int8_t* __restrict__ dn, int B,
+                                                                   int Zc, int zi, int64_t ldk,
+                                                                   int64_t ldn) {
+    int b = blockIdx.x;
+    if (b >= B) return;
+    const int t = threadIdx.x;
+    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
+    const int twoZ = 2 * Zc, KW = Ly.KW;
+    extern __shared__ __align__(16) uint32_t sm[];
+    int4 buf[2][2];
+    auto load = [&](int cb) {
+        const int8_t* src = ck + (int64_t)cb * ldk;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int wi = t + c * kEncPipeNT;
+            if (wi < KW) {
+                buf[c][0] = *(const int4*)(src + wi * 32);
+                buf[c][1] = *(const int4*)(src + wi * 32 + 16);
+            }
+        }
+    };
+    load(b);
+    for (; b < B; b += gridDim.x) {
+        int8_t* dst = dn + (int64_t)b * ldn;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int wi = t + c * kEncPipeNT;
+            if (wi < KW) sm[wi] = enc_pack_chunk(buf[c], wi * 32, twoZ, dst);
+        }
+        if (t < 2) sm[KW + t] = 0;
+        if (b + (int)gridDim.x < B) load(b + gridDim.x);
+        lds_sync();
+        enc_fast_parity<BG, true>(Ly, sm, dst, Zc, zi, t, kEncPipeNT);
+        lds_sync();   // ib / X / lam / pv are rewritten by the next codeblock
+    }
+}
 }  // namespace
 
 int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,
@@ -434,17 +485,51 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
     const bool fast = (Zc % 16) == 0 && (ldk % 16) == 0 && (ldn % 16) == 0 &&
                       (((uintptr_t)ck) & 15) == 0 && (((uintptr_t)dn) & 15) == 0;
     if (fast) {
+        // LDPC5G_ENC_MODE (A/B switch): pipe (default) | fast | sync (fast with full barriers)
+        static const int mode = [] {
+            const char* e = getenv("LDPC5G_ENC_MODE");
+            if (e && !strcmp(e, "fast")) return 1;
+            if (e && !strcmp(e, "sync")) return 2;
+            return 0;
+        }();
         static const int nt = [] {
             const char* e = getenv("LDPC5G_ENC_THREADS");
             int v = e ? atoi(e) : 128;
             return (v == 64 || v == 128 || v == 256) ? v : 128;
         }();
-        if (bgn == 1)
-            hipLaunchKernelGGL(ldpc_enc_fast_kernel<1>, dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
-                               st, ck, dn, B, Zc, zi, ldk, ldn);
-        else
-            hipLaunchKernelGGL(ldpc_enc_fast_kernel<2>, dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
-                               st, ck, dn, B, Zc, zi, ldk, ldn);
+        if (mode == 0) {
+            static const int per_cu = [] {
+                const char* e = getenv("LDPC5G_ENC_WG_PER_CU");
+                int v = e ? atoi(e) : 4;
+                return v >= 1 && v <= 16 ? v : 4;
+            }();
+            int dev = 0, ncu = 256;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            const int grid = std::min(B, ncu * per_cu);
+            if (bgn == 1)
+                hipLaunchKernelGGL(ldpc_enc_pipe_kernel<1>, dim3(grid), dim3(kEncPipeNT),
+                                   enc_fast_lds_bytes<1>(Zc), st, ck, dn, B, Zc, zi, ldk, ldn);
+            else
+                hipLaunchKernelGGL(ldpc_enc_pipe_kernel<2>, dim3(grid), dim3(kEncPipeNT),
+                                   enc_fast_lds_bytes<2>(Zc), st, ck, dn, B, Zc, zi, ldk, ldn);
+            return check_hip(hipGetLastError(), "ldpc_enc_pipe_kernel launch");
+        }
+        if (mode == 1) {
+            if (bgn == 1)
+                hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
+                                   st, ck, dn, B, Zc, zi, ldk, ldn);
+            else
+                hipLaunchKernelGGL((ldpc_enc_fast_kernel<2, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
+                                   st, ck, dn, B, Zc, zi, ldk, ldn);
+        } else {
+            if (bgn == 1)
+                hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, false>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
+                                   st, ck, dn, B, Zc, zi, ldk, ldn);
+            else
+                hipLaunchKernelGGL((ldpc_enc_fast_kernel<2, false>), dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
+                                   st, ck, dn, B, Zc, zi, ldk, ldn);
+        }
         return check_hip(hipGetLastError(), "ldpc_enc_fast_kernel launch");
     }
     if (bgn == 1)

@@ -41,3 +41,47 @@ def decode_mixed(items, L, alpha=1.0, beta=0.0, schedule="flooding"):
     ckh = ck.cpu().numpy()
     return ([ckh[c:c + n].copy() for _, c, n in rows], st.cpu().numpy()[:B].astype(bool),
             it.cpu().numpy()[:B])
+
+
+class MixedBatch:
+    """A device-resident mixed-(bgn, Zc) batch for repeated decoding (the bench's config 4):
+    rows of several (bgn, Zc) groups concatenated in one flat float32 LLR buffer, with the
+    descriptor array (ldpc5g_cb_desc_t) built once.
+
+    groups: list of (bgn, Zc, llr (n, N) float32 device tensor)."""
+
+    def __init__(self, groups):
+        t = _lib.require_gpu()
+        B = sum(g[2].shape[0] for g in groups)
+        self.desc = (_lib.CbDesc * max(B, 1))()
+        parts, lo, co, k = [], 0, 0, 0
+        self.rows = []
+        for bgn, Zc, llr in groups:
+            assert bgn in [1, 2] and find_iLS(Zc) < 8 and llr.dtype == t.float32
+            K, N, Nf = code_dims(bgn, Zc)
+            assert llr.dim() == 2 and llr.shape[1] == N
+            for _ in range(llr.shape[0]):
+                d = self.desc[k]
+                d.bgn, d.Zc, d.llr_off, d.ck_off = bgn, Zc, lo, co
+                self.rows.append((co, Nf))
+                lo += N
+                co += Nf
+                k += 1
+            parts.append(llr.reshape(-1))
+        dev = groups[0][2].device
+        self.llr = t.cat(parts).contiguous()
+        self.ck = t.empty(max(co, 1), dtype=t.int8, device=dev)
+        self.status = t.empty(max(B, 1), dtype=t.uint8, device=dev)
+        self.iters = t.empty(max(B, 1), dtype=t.int32, device=dev)
+        self.B = B
+
+    def decode(self, L, alpha=1.0, beta=0.0, schedule="layered"):
+        """One ldpc5g_decode_ms_mixed call (<= 2 kernel launches; returns after they finish)."""
+        t = _lib.torch()
+        with t.cuda.device(self.llr.device):
+            _lib.check(_lib.lib().ldpc5g_decode_ms_mixed(
+                self.desc, self.B, _lib.ptr(self.llr), _lib.F32, _lib.ptr(self.ck),
+                _lib.ptr(self.status), _lib.ptr(self.iters), int(L), float(alpha), float(beta),
+                _lib.LAYERED if schedule == "layered" else _lib.FLOODING, 0,
+                _lib.stream_ptr(self.llr.device)))
+        return self.ck, self.status[:self.B], self.iters[:self.B]

@@ -1,26 +1,72 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprof kernel-trace summary.
-# Usage (from the repo root, via gpurun):  bash tools/gpu_round.sh [tag]
-# Every GPU step has its own time limit; the first failure ends the script.
-set -euo pipefail
+# One GPU-box session: parity tests, smoke, bench, rocprof kernel trace, encoder A/B probes and
+# PMC counter passes.  Usage (from the repo root, via gpurun):  bash tools/gpu_round.sh TAG [steps]
+#   steps: comma list of {tests,smoke,bench,trace,probe,pmc}; default all.
+# Every GPU step has its own time limit.  A test FAILURE (pytest rc 1) does not stop the script;
+# a crash, abort or time limit (any other non-zero rc) ends it at once.
+set -uo pipefail
 TAG=${1:-run}
+STEPS=${2:-tests,smoke,bench,trace,probe,pmc}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-echo "[gpu_round] tests"
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-    > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
-tail -3 "$OUT/pytest_gpu.log"
-echo "[gpu_round] smoke"
-timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
-tail -2 "$OUT/smoke.log"
-echo "[gpu_round] bench"
-timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-cat "$OUT/bench.json"
-echo "[gpu_round] rocprof kernel trace"
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-    python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err"
-cd "$ROOT"
-find "$OUT/prof" -name '*kernel_stats.csv' -exec head -8 {} \;
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+die() { echo "[gpu_round] $1 failed rc=$2 — stopping"; exit "$2"; }
+
+if has tests; then
+  echo "[gpu_round] tests"
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread \
+      > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?
+  tail -5 "$OUT/pytest_gpu.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then die tests $rc; fi
+  if [ $rc -eq 1 ]; then grep -E "^(FAILED|ERROR)|Error" "$OUT/pytest_gpu.log" | head -20; fi
+fi
+if has smoke; then
+  echo "[gpu_round] smoke"
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || die smoke $?
+  tail -1 "$OUT/smoke.log"
+fi
+if has bench; then
+  echo "[gpu_round] bench"
+  timeout -k 10 420 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; die bench $?; }
+  cat "$OUT/bench.json"
+fi
+if has trace; then
+  echo "[gpu_round] rocprof kernel trace"
+  cd /tmp
+  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+      python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
+      || { tail -20 "$OUT/rocprof.err"; die trace $?; }
+  cd "$ROOT"
+  python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
+  cut -c1-150 "$OUT/kernel_stats.csv" | head -12
+fi
+if has probe; then
+  echo "[gpu_round] encoder A/B"
+  for m in pipe fast sync; do
+    LDPC5G_ENC_MODE=$m timeout -k 10 120 python -u tools/probe.py encode 4096 16384 > "$OUT/probe_enc_$m.log" 2>&1 || die probe $?
+    echo "$m: $(tr '\n' ' ' < "$OUT/probe_enc_$m.log")"
+  done
+  for w in 2 8; do
+    LDPC5G_ENC_WG_PER_CU=$w timeout -k 10 120 python -u tools/probe.py encode 4096 > "$OUT/probe_enc_pipe_w$w.log" 2>&1 || die probe $?
+    echo "pipe w$w: $(cat "$OUT/probe_enc_pipe_w$w.log")"
+  done
+fi
+if has pmc; then
+  echo "[gpu_round] PMC passes"
+  cd /tmp
+  i=0
+  for ctr in "FETCH_SIZE" "WRITE_SIZE" \
+             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
+             "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+    i=$((i + 1))
+    timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc$i" -o run -- \
+        python -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-extras \
+        > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || { tail -5 "$OUT/pmc$i.err"; cd "$ROOT"; die "pmc $ctr" $?; }
+  done
+  cd "$ROOT"
+  python tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.json" && cat "$OUT/pmc_summary.json"
+fi
+echo "[gpu_round] done"
