@@ -117,6 +117,12 @@ constexpr bool xl_lds() { return sizeof(T) == 4 && !LAYERED; }
 // are held to fewer resident waves).  2 x (40 KB APP + 33 KB state + 3 KB flags) <= 160 KB.
 template <int BG>
 constexpr int lds_rows() { return BG == 1 ? 11 : 18; }
+// Layered rows with more edges than this recompute their rotated LDS addresses in pass 2
+// (LDPC5G_RECOMP_DEG overrides it at build time for A/B builds).
+#ifndef LDPC5G_RECOMP_DEG
+#define LDPC5G_RECOMP_DEG 12
+#endif
+constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
 // LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
 template <bool LAYERED>
 constexpr int dec_cs() { return LAYERED ? kDecThreadsL : kDecThreads; }
@@ -430,6 +436,16 @@ __device__ __forceinline__ void dec_body(
             const T nAs = FT<T>::xsign(alpha * (x1 > T(0) ? x1 : T(0)), sx);
             const T nBs = FT<T>::xsign(alpha * (x2 > T(0) ? x2 : T(0)), sx);
             uint32_t negs = 0, idxn = 0;
+            // High-degree rows (BG1 rows 0-3, d = 19): keeping all d rotated addresses live from
+            // pass 1 to pass 2 beside the d messages overflows the 168-VGPR budget (scratch spills
+            // reloaded inside the iteration loop); their addresses are recomputed from an opaque
+            // copy of the thread offsets instead (2 VALU per edge, no CSE with pass 1).
+            constexpr bool RECOMP = d > kRecompDeg;
+            uint32_t tzb2 = (uint32_t)tzb, tzbw2 = tzbw;
+            if constexpr (RECOMP) {
+                asm volatile("" : "+v"(tzb2));
+                asm volatile("" : "+v"(tzbw2));
+            }
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
@@ -440,8 +456,16 @@ __device__ __forceinline__ void dec_body(
                 const T r = __uint_as_float(__builtin_amdgcn_bitop3_b32(qb, __float_as_uint(sel), mv, 0x6c));
                 negs = __builtin_amdgcn_alignbit(negs, qb, 31);
                 const T app = q[k] + r;
-                if constexpr (j < KC) at(j * CS * TS + rb[k]) = app;
-                else hdx |= (uint64_t)(app < T(0)) << (i - 4);
+                if constexpr (j < KC) {
+                    if constexpr (RECOMP) {
+                        const uint32_t S = (uint32_t)gshift(e0 + k) * GT;
+                        at(j * CS * TS + (int)min(tzb2 + S, tzbw2 + S)) = app;
+                    } else {
+                        at(j * CS * TS + rb[k]) = app;
+                    }
+                } else {
+                    hdx |= (uint64_t)(app < T(0)) << (i - 4);
+                }
             });
             putAB(ic, nAs, nBs);
             put_row(ic, negs, idxn);

@@ -485,12 +485,15 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
     const bool fast = (Zc % 16) == 0 && (ldk % 16) == 0 && (ldn % 16) == 0 &&
                       (((uintptr_t)ck) & 15) == 0 && (((uintptr_t)dn) & 15) == 0;
     if (fast) {
-        // LDPC5G_ENC_MODE (A/B switch): pipe (default) | fast | sync (fast with full barriers)
+        // LDPC5G_ENC_MODE (A/B switch): fast (default) | pipe | sync (fast with full barriers).
+        // Measured (r01c, 4096 x BG1 Zc=384): fast 40.2 us, sync 40.4 us, pipe 62.5 us (4 WG/CU),
+        // 61.1 us (8 WG/CU): the per-codeblock LDS/VALU critical path, not HBM, sets the time, so
+        // the most codeblocks in flight (one per workgroup) wins.
         static const int mode = [] {
             const char* e = getenv("LDPC5G_ENC_MODE");
-            if (e && !strcmp(e, "fast")) return 1;
+            if (e && !strcmp(e, "pipe")) return 0;
             if (e && !strcmp(e, "sync")) return 2;
-            return 0;
+            return 1;
         }();
         static const int nt = [] {
             const char* e = getenv("LDPC5G_ENC_THREADS");

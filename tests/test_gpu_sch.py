@@ -196,7 +196,7 @@ def test_sch_decode_batch_matches_per_tb_and_oracle(torch, sch):
     T = 6
     tb = rng.integers(0, 2, (T, A)).astype(np.int8)
     g = sch.sch_encode_batch(torch.from_numpy(tb).cuda(), cfg).cpu().numpy()
-    snrs = [4.0, 4.0, 2.0, 1.0, 0.0, -2.0]
+    snrs = [9.0, 9.0, 3.0, 1.0, 0.0, -2.0]
     llr = np.stack([O.bpsk_awgn_llr(g[t], snrs[t], rng) for t in range(T)])
     x = torch.from_numpy(llr).cuda()
     r = sch.sch_decode_batch(x, cfg, 5, "min-sum", 0.75, 0.0, "flooding")
@@ -210,7 +210,7 @@ def test_sch_decode_batch_matches_per_tb_and_oracle(torch, sch):
         ok, blk, cbok = O.sch_tb_check(ck, p)
         assert tb_ok[t] == ok and np.array_equal(tbblk[t, :A], blk), t
         assert np.array_equal(r.cb_crc_ok.cpu().numpy()[t * cfg.C:(t + 1) * cfg.C].astype(bool), cbok)
-    assert tb_ok[:2].all()   # high SNR decodes
+    assert tb_ok[:2].all() and not tb_ok[-1]   # 9 dB decodes, -2 dB does not
     # layered float32
     r2 = sch.sch_decode_batch(x.float(), cfg, 5, "min-sum", 0.75, 0.0, "layered")
     dn32 = r2.llr_dn.cpu().numpy()
