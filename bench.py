@@ -27,6 +27,26 @@ EDGES = 316 * ZC
 DEC_BYTES_PER_CB = 4 * N_TX + N_FULL + 1 + 4       # f32 LLR in, int8 ck out, status, iters
 ENC_BYTES_PER_CB = K_INFO + N_TX                     # int8 bits in, int8 dn out
 HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip table (spec)
+# rocprofv3 PMC summary of this code version (tools/gpu_round.sh pmc step -> tools/pmc_summary.py),
+# committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true>",
+              "flooding": "void ldpc_dec_kernel<1, float, false>"}
+ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
+
+
+def pmc_traffic(kernel, corrected16=False):
+    """HBM bytes per launch of `kernel` (4096-codeblock batch) from the committed PMC summary,
+    or None.  corrected16: FETCH_SIZE doubled for 16-B/lane streaming loads (MI355X_MICROARCH.md
+    §HBM); the decoder's 4-B loads are uncalibrated and reported raw."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            e = json.load(f)["kernels"][kernel]
+        return int(e["hbm_bytes_fetch16_corrected" if corrected16 else "hbm_bytes_raw"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12        # 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T/s
 
 
@@ -172,7 +192,7 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     ws = SchWorkspace(cfg, T, dev)
     wt, _ = timed(torch, dist, world, lambda: sch_encode_batch(tb, cfg, ws), steps, 2)
     gs = sch_encode_batch(tb, cfg, ws)
-    snr = 6.0
+    snr = 8.0   # the rate-0.95 codeblocks need ~8 dB (BPSK) to decode in 8 iterations
     sigma = 10 ** (-snr / 20)
     llr = (2 * ((1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g))
            / sigma ** 2).contiguous()
@@ -251,8 +271,12 @@ def main():
                    "converged": conv, "parallelism": f"cb-shard x{world}"},
         "info_gbit_s": round(value * K_INFO / 1e9, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": f"ldpc_dec_kernel<1,float,{args.schedule == 'layered'}>",
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": pmc_traffic(DEC_KERNEL[args.schedule]) if B == 4096 else None,
+                     "traffic_source": "profiles/pmc_latest.json: FETCH_SIZE + WRITE_SIZE bytes "
+                                       "per 4096-CB launch (raw; FETCH includes Infinity-Cache "
+                                       "hits of the per-iteration ext-column LLR re-reads)",
+                     "kernel": DEC_KERNEL[args.schedule],
                      "algorithmic_bytes_per_cb": DEC_BYTES_PER_CB,
                      "launch_ms": round(launch_s * 1e3, 4),
                      "note": "decode is VALU/LDS-bound (~99 lane-op/B); see valu"},
@@ -297,6 +321,9 @@ def main():
                                 "roofline": {"bound": "hbm", "achieved": round(ach, 1),
                                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                              "frac": round(ach / HBM_PEAK_GBS, 4),
+                                             "traffic": pmc_traffic(ENC_KERNEL, True)
+                                             if B == 4096 else None,
+                                             "kernel": ENC_KERNEL,
                                              "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB}}
         ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2))
         ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
