@@ -179,9 +179,11 @@ def bench_config4(torch, dist, world, dev, rank, steps):
 
 def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     """BASELINE config 5: PDSCH 273 PRB 256QAM MCS27 4 layers TB stream (TBS 1,081,512 ->
-    129 BG1 Zc=384 codeblocks per TB, G = 8*4*36036), T TBs per GPU: the GPU DL-SCH chain both
-    ways (ldpc5g_sch_encode; ldpc5g_sch_decode = rate recovery + layered NMS L=8 + CB/TB CRCs),
-    LLRs from BPSK + AWGN on the rate-matched bits (no modem: the chain's input is LLRs)."""
+    129 BG1 Zc=384 codeblocks per TB, G = 8*4*36036), T TBs per GPU, every step on the GPU:
+    TX = ldpc5g_sch_encode + scrambling/256QAM mapping; RX = soft demodulation/descrambling +
+    ldpc5g_sch_decode (rate recovery, layered NMS L=8, CB/TB CRCs).  Channel: complex AWGN on the
+    symbols at 30 dB (outside the timed regions)."""
+    from python_5gtoolbox_amd import phy
     from python_5gtoolbox_amd.sch import SchWorkspace, sch_config, sch_decode_batch, \
         sch_encode_batch
     A, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
@@ -189,21 +191,32 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     g = torch.Generator(device=dev)
     g.manual_seed(505 + rank)
     tb = torch.randint(0, 2, (T, A), dtype=torch.int8, device=dev, generator=g)
+    cinit = (torch.arange(T, device=dev, dtype=torch.int64) + 1000 * rank) * 2 ** 15 + 7
     ws = SchWorkspace(cfg, T, dev)
-    wt, _ = timed(torch, dist, world, lambda: sch_encode_batch(tb, cfg, ws), steps, 2)
-    gs = sch_encode_batch(tb, cfg, ws)
-    snr = 8.0   # the rate-0.95 codeblocks need ~8 dB (BPSK) to decode in 8 iterations
-    sigma = 10 ** (-snr / 20)
-    llr = (2 * ((1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g))
-           / sigma ** 2).contiguous()
+    sym = torch.empty((T, G // Qm), dtype=torch.complex64, device=dev)
+
+    def tx():
+        bits = sch_encode_batch(tb, cfg, ws)
+        phy.scramble_modulate(bits, Qm, cinit, out=sym)
+    wt, _ = timed(torch, dist, world, tx, steps, 2)
+    tx()
+    snr = 30.0
+    nvar = 10 ** (-snr / 10)
+    noise = torch.complex(torch.randn(sym.shape, device=dev, generator=g),
+                          torch.randn(sym.shape, device=dev, generator=g)) * (nvar / 2) ** 0.5
+    y = (sym + noise).contiguous()
+    del noise
+    nv = torch.full(sym.shape, nvar, dtype=torch.float32, device=dev)
+    llr = torch.empty((T, G), dtype=torch.float32, device=dev)
 
     def rx():
-        sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+        phy.demod_descramble(y, nv, Qm, cinit, out=llr)
+        return sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
     wr, _ = timed(torch, dist, world, rx, steps, 2)
-    r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+    r = rx()
     ok = bool(torch.equal(r.tbblk[:, :A], tb))
-    return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, BG1 Zc=384, "
-                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), snr {snr} dB BPSK-AWGN LLRs",
+    return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, 256QAM, BG1 Zc=384, "
+                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN {snr} dB",
             "tb_per_gpu": T, "codeblocks_per_tb": cfg.C,
             "rx_tb_per_s": round(T * world * steps / wr, 2),
             "rx_codeblocks_per_s": round(T * cfg.C * world * steps / wr, 1),

@@ -192,6 +192,33 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
                       int32_t schedule, int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok,
                       uint32_t* tb_rem, uint8_t* tb_ok, void* stream);
 
+/* ================================================ scrambling, modulation, soft demodulation
+ * The symbol-level steps either side of the DL-SCH chain (TS 38.211 5.2.1, 5.1, 7.3.1.1-2),
+ * batched over T transport blocks with one scrambling init each.  Packed bit words: bit k of
+ * word w = element 32w + k. */
+
+/* gen_nrPRBS (py5gphy/common/nrPRBS.py:5-25) of every TB: words [T][ldw] uint32 receive
+ * c(0 .. nbits-1) for c_init = cinit[t] (cinit: DEVICE array of T values). */
+int ldpc5g_prbs(const uint32_t* cinit, int32_t T, int64_t nbits, uint32_t* words, int64_t ldw,
+                void* stream);
+
+/* Scrambling + modulation mapper (nr_pdsch_process.py:17-25, nrModulation.py:4-41), Qm = 2, 4,
+ * 6, 8 (QPSK..256QAM): bits [T][ldb] int8 (nbits each) XOR prbs words (NULL: no scrambling) ->
+ * complex64 symbols [T][ldsym] (float2), bit-exact with the reference's float32 arithmetic. */
+int ldpc5g_scramble_modulate(const int8_t* bits, int64_t ldb, const uint32_t* prbs, int64_t ldw,
+                             int32_t T, int64_t nbits, int32_t Qm, void* sym, int64_t ldsym,
+                             void* stream);
+
+/* Soft demodulation (nr_Demodulation.py:12-46, demod_{qpsk,16qam,64qam,256qam}.py) + LLR
+ * descrambling (nr_pdsch.py:268-274): symbols [T][ldsym] complex64 (LDPC5G_F32) or complex128
+ * (LDPC5G_F64), noise variances [T][ldnv] float32 -> LLRs [T][ldllr] float32 (nsym*Qm each),
+ * multiplied by 1 - 2c(n) when prbs is not NULL.  float64 arithmetic in the reference's order:
+ * bit-exact with the reference on complex128 input. */
+int ldpc5g_demod_descramble(const void* sym, int32_t sym_dtype, int64_t ldsym,
+                            const float* noise_var, int64_t ldnv, const uint32_t* prbs,
+                            int64_t ldw, int32_t T, int64_t nsym, int32_t Qm, float* llr,
+                            int64_t ldllr, void* stream);
+
 /* Message of the last failed call on this thread ("" if none). */
 const char* ldpc5g_last_error(void);
 

@@ -670,3 +670,98 @@ def sch_tb_check(ck, p):
         tb[c * cbz:(c + 1) * cbz] = ck[c, :cbz]
     blk, err = crc_decode(tb, p["poly"])
     return err == 0, blk, cb_ok
+
+
+# ------------------------------------- scrambling, modulation, soft demodulation
+def prbs(c_init, N):
+    """gen_nrPRBS (py5gphy/common/nrPRBS.py:5-25): Gold sequence c(n) = x1(n+1600) + x2(n+1600)
+    mod 2; x1 = 1,0,..,0, x2 = bits of c_init; x1(n+31) = x1(n+3)+x1(n),
+    x2(n+31) = x2(n+3)+x2(n+2)+x2(n+1)+x2(n).  Generated 28 bits per step (the recurrences
+    only reach back 31 - 3 = 28 positions)."""
+    assert N > 0
+    L = 1600 + N + 31
+    x1 = np.zeros(L + 28, np.int8)
+    x2 = np.zeros(L + 28, np.int8)
+    x1[0] = 1
+    x2[:31] = [(c_init >> i) & 1 for i in range(31)]
+    for m in range(0, L - 31, 28):
+        x1[m + 31:m + 59] = x1[m + 3:m + 31] ^ x1[m:m + 28]
+        x2[m + 31:m + 59] = x2[m + 3:m + 31] ^ x2[m + 2:m + 30] ^ x2[m + 1:m + 29] ^ x2[m:m + 28]
+    return (x1[1600:1600 + N] ^ x2[1600:1600 + N]).astype(np.int8)
+
+
+_QAM_SCALE = {2: 2, 4: 10, 6: 42, 8: 170}
+
+
+def modulate(bits, Qm):
+    """nrModulate (py5gphy/common/nrModulation.py:4-41) for QPSK..256QAM: float32 levels, then
+    numpy's complex64 division by the real scalar sqrt(scale), which multiplies by the float32
+    reciprocal 1 / float32(sqrt(scale)) (Smith's algorithm with a zero imaginary divisor)."""
+    b = np.asarray(bits).astype(np.float32).reshape(-1, Qm)
+    u = 1 - 2 * b                                   # float32
+    if Qm == 2:
+        re, im = u[:, 0], u[:, 1]
+    elif Qm == 4:
+        re, im = u[:, 0] * (2 - u[:, 2]), u[:, 1] * (2 - u[:, 3])
+    elif Qm == 6:
+        re = u[:, 0] * (4 - u[:, 2] * (2 - u[:, 4]))
+        im = u[:, 1] * (4 - u[:, 3] * (2 - u[:, 5]))
+    else:
+        re = u[:, 0] * (8 - u[:, 2] * (4 - u[:, 4] * (2 - u[:, 6])))
+        im = u[:, 1] * (8 - u[:, 3] * (4 - u[:, 5] * (2 - u[:, 7])))
+    scl = np.float32(1) / np.float32(math.sqrt(_QAM_SCALE[Qm]))
+    return (re * scl + 1j * (im * scl)).astype(np.complex64)
+
+
+# Piecewise-linear soft-demodulation segments of demod_{qpsk,16qam,64qam,256qam}.py, per PAM
+# bit pair p (bits 2p / 2p+1 from the real / imaginary part): (upper threshold in units of A,
+# k, s, c) meaning  r < thr*A  ->  LLR = (k*A) * (s*r + (s*c)*A) / noise_var  (= s (k A)(r + c A)
+# / noise_var up to the sign of zero, which follows the reference's written form; c = 0: (k*A)*r).
+_INF = float("inf")
+DEMOD_SEGMENTS = {
+    2: [[(_INF, 4, 1, 0)]],
+    4: [[(-2, 8, 1, 1), (2, 4, 1, 0), (_INF, 8, 1, -1)],
+        [(0, 4, 1, 2), (_INF, 4, -1, -2)]],
+    6: [[(-6, 16, 1, 3), (-4, 12, 1, 2), (-2, 8, 1, 1), (2, 4, 1, 0), (4, 8, 1, -1),
+         (6, 12, 1, -2), (_INF, 16, 1, -3)],
+        [(-6, 8, 1, 5), (-2, 4, 1, 4), (0, 8, 1, 3), (2, 8, -1, -3), (6, 4, -1, -4),
+         (_INF, 8, -1, -5)],
+        [(-4, 4, 1, 6), (0, 4, -1, 2), (4, 4, 1, -2), (_INF, 4, -1, -6)]],
+    8: [[(-14, 32, 1, 7), (-12, 28, 1, 6), (-10, 24, 1, 5), (-8, 20, 1, 4), (-6, 16, 1, 3),
+         (-4, 12, 1, 2), (-2, 8, 1, 1), (2, 4, 1, 0), (4, 8, 1, -1), (6, 12, 1, -2),
+         (8, 16, 1, -3), (10, 20, 1, -4), (12, 24, 1, -5), (14, 28, 1, -6), (_INF, 32, 1, -7)],
+        [(-14, 16, 1, 11), (-12, 12, 1, 10), (-10, 8, 1, 9), (-6, 4, 1, 8), (-4, 8, 1, 7),
+         (-2, 12, 1, 6), (0, 16, 1, 5), (2, 16, -1, -5), (4, 12, -1, -6), (6, 8, -1, -7),
+         (10, 4, -1, -8), (12, 8, -1, -9), (14, 12, -1, -10), (_INF, 16, -1, -11)],
+        [(-14, 8, 1, 13), (-10, 4, 1, 12), (-8, 8, 1, 11), (-6, 8, -1, 5), (-2, 4, -1, 4),
+         (0, 8, -1, 3), (2, 8, 1, -3), (6, 4, 1, -4), (8, 8, 1, -5), (10, 8, -1, -11),
+         (14, 4, -1, -12), (_INF, 8, -1, -13)],
+        [(-12, 4, 1, 14), (-8, 4, -1, 10), (-4, 4, 1, 6), (0, 4, -1, 2), (4, 4, 1, -2),
+         (8, 4, -1, -6), (12, 4, 1, -10), (_INF, 4, -1, -14)]],
+}
+
+
+def demodulate(sym, noise_var, Qm):
+    """nrDemodulate (demodulation/nr_Demodulation.py:12-46 -> demod_*.py) for QPSK..256QAM:
+    float64 arithmetic in the reference's operation order, stored as float32."""
+    y = np.asarray(sym, np.complex128).reshape(-1)
+    nv = np.asarray(noise_var).real.reshape(-1).astype(np.float32).astype(np.float64)
+    A = 1 / math.sqrt(_QAM_SCALE[Qm])
+    out = np.zeros(y.size * Qm, np.float32)
+    for p, segs in enumerate(DEMOD_SEGMENTS[Qm]):
+        thr = np.array([t * A if t != _INF else _INF for t, _, _, _ in segs[:-1]])
+        for part, r in ((0, y.real), (1, y.imag)):
+            reg = np.searchsorted(thr, r, side="right")
+            v = np.zeros(r.size)
+            for i, (_, k, s, c) in enumerate(segs):
+                m = reg == i
+                x = r[m] if c == 0 else s * r[m] + (s * c) * A
+                v[m] = ((k * A) * x) / nv[m]
+            out[2 * p + part::Qm] = v
+    return out
+
+
+def descramble(llr, c_init):
+    """nr_pdsch.py:268-274: LLR * (1 - 2 c(n))."""
+    llr = np.asarray(llr)
+    return llr * (1 - 2 * prbs(c_init, llr.size)).astype(llr.dtype)

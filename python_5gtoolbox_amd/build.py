@@ -49,6 +49,7 @@ def up_to_date():
 def _compile(src, verbose, obj_dir=None, csrc=CSRC):
     obj = os.path.join(obj_dir or OBJ, os.path.basename(src) + ".o")
     flags = [f for f in FLAGS if f != f"-I{CSRC}"] + [f"-I{csrc}"]
+    flags += os.environ.get("LDPC5G_EXTRA_FLAGS", "").split()   # A/B builds (-D...)
     if os.path.basename(src) in NO_SLP and not os.environ.get("LDPC5G_SLP"):
         flags.append("-fno-slp-vectorize")
     cmd = [HIPCC, *flags, "-c", src, "-o", obj]
@@ -59,14 +60,14 @@ def _compile(src, verbose, obj_dir=None, csrc=CSRC):
 
 
 def build(force=False, verbose=True, csrc=None, out=None):
-    alt = csrc is not None
+    alt = csrc is not None or out is not None
     lib_path = out or LIB
     if not alt and not force and up_to_date():
         if verbose:
             print("libldpc5g.so up to date")
         return LIB
     csrc = csrc or CSRC
-    obj_dir = os.path.join(ROOT, "build", "obj_alt" if alt else "obj")
+    obj_dir = os.path.join(ROOT, "build", ("obj_alt_" + os.path.basename(lib_path)) if alt else "obj")
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:

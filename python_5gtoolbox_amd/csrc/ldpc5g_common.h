@@ -96,7 +96,10 @@ constexpr int kCS = kDecThreads;   // LDS column stride (entries): G*Zc <= 384 a
 
 // layered float32 kernel: 768-thread workgroups (12 waves = 3 per SIMD at <= 168 VGPRs) holding
 // G = floor(768 / Zc) codeblocks, e.g. two BG1 Zc=384 codeblocks
-constexpr int kDecThreadsL = 768;
+#ifndef LDPC5G_LAYERED_THREADS
+#define LDPC5G_LAYERED_THREADS 768   // A/B builds: -DLDPC5G_LAYERED_THREADS=384 (1 CB/workgroup, 2 workgroups/CU)
+#endif
+constexpr int kDecThreadsL = LDPC5G_LAYERED_THREADS;
 inline int dec_threads(bool layered) { return layered ? kDecThreadsL : kDecThreads; }
 inline int dec_G(int Zc, bool layered = false) {
     const int T = dec_threads(layered);

@@ -16,6 +16,7 @@ the float64 widening of those float32 values so the fixtures are exact for both 
   crc_golden.json      CRC KATs (the inline vectors of py5gphy/crc/crc.py:167-210) + generated
   dlsch_golden.npz     DLSCHEncode (nr_dlsch.py:12) transport blocks -> g_seq
   sch_golden.npz/.json DLSCHDecode (+HARQ), ULSCH encode/decode, a config-5 DLSCHEncode TB
+  demod_golden.npz     nrModulate / nrDemodulate (QPSK..256QAM) / gen_nrPRBS vectors
   decode_bf_golden.npz / decode_bp_golden.npz   nr_decode_ldpc with algo='BF' / 'BP'
 """
 import json
@@ -388,10 +389,48 @@ def gen_sch():
     print("sch cases", len(cases))
 
 
+# ------------------------------------------------------- modulation / demodulation / PRBS (f4)
+def gen_demod():
+    """nrModulate (common/nrModulation.py:4-41), nrDemodulate (demodulation/nr_Demodulation.py:
+    12-46) for QPSK..256QAM, gen_nrPRBS (common/nrPRBS.py:5-25)."""
+    from py5gphy.common import nrModulation, nrPRBS
+    from py5gphy.demodulation import nr_Demodulation
+    rng = np.random.default_rng(17)
+    blobs, meta = {}, []
+    for k, (mod, Qm, scale) in enumerate([("qpsk", 2, 2), ("16qam", 4, 10), ("64qam", 6, 42),
+                                          ("256qam", 8, 170)]):
+        n = 3000
+        bits = rng.integers(0, 2, n * Qm)
+        sym = nrModulation.nrModulate(bits, mod)
+        A = 1 / np.sqrt(scale)
+        # noisy symbols + exact decision-threshold values (multiples of A) + zeros
+        y = sym.astype(np.complex128) + (rng.normal(0, 0.3, n) + 1j * rng.normal(0, 0.3, n)) * A * 3
+        th = rng.integers(-16, 17, 400) * A
+        y[:400] = th + 1j * th[::-1]
+        y[400:410] = 0.0
+        nv = rng.uniform(0.01, 1.0, n)
+        _, llr = nr_Demodulation.nrDemodulate(y, mod, nv)
+        blobs[f"bits{k}"] = np.packbits(bits.astype(np.uint8))
+        blobs[f"sym{k}"] = np.asarray(sym)                      # reference modulation output
+        blobs[f"y{k}"] = y
+        blobs[f"nv{k}"] = nv.astype(np.float32)
+        blobs[f"llr{k}"] = np.asarray(llr, np.float32)
+        meta.append((Qm, n))
+    prbs = []
+    for j, (cinit, N) in enumerate([(0, 64), (1, 1000), (12345 * 2 ** 15 + 7, 100003),
+                                    (2 ** 31 - 1, 4096), (65535 * 2 ** 15 + 1023, 1153152)]):
+        seq = nrPRBS.gen_nrPRBS(cinit, N)
+        blobs[f"prbs{j}"] = np.packbits(seq.astype(np.uint8))
+        prbs.append((cinit, N))
+    np.savez_compressed(os.path.join(OUT, "demod_golden.npz"), meta=np.array(meta, np.int64),
+                        prbs_meta=np.array(prbs, np.int64), **blobs)
+    print("demod cases", len(meta), "prbs cases", len(prbs))
+
+
 if __name__ == "__main__":
     os.chdir(REF)
     sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
-    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "decode", "bfbp"]
+    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "demod", "decode", "bfbp"]
     if "encode" in which:
         gen_encode()
     if "crc" in which:
@@ -402,6 +441,8 @@ if __name__ == "__main__":
         gen_dlsch()
     if "sch" in which:
         gen_sch()
+    if "demod" in which:
+        gen_demod()
     if "decode" in which:
         with mp.get_context("fork").Pool(6) as pool:
             gen_decode(pool)

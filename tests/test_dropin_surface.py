@@ -25,6 +25,9 @@ PAIRS = [
     ("nr_pusch/nr_ulsch.py", "python_5gtoolbox_amd.nr_ulsch",
      ["ULSCH_Crc_CodeBlockSegment", "ULSCH_encoding_ratematch"]),
     ("nr_pusch/nr_ulsch_decode.py", "python_5gtoolbox_amd.nr_ulsch_decode", ["ULSCH_decoding"]),
+    ("common/nrPRBS.py", "python_5gtoolbox_amd.nrPRBS", ["gen_nrPRBS"]),
+    ("common/nrModulation.py", "python_5gtoolbox_amd.nrModulation", ["nrModulate"]),
+    ("demodulation/nr_Demodulation.py", "python_5gtoolbox_amd.nr_Demodulation", ["nrDemodulate"]),
 ]
 
 

@@ -153,3 +153,16 @@ def test_bf_bp_golden(algo):
     for c in load_algo_cases(algo):
         ck, st, _ = fn(c["llr"][None].astype(np.float64), c["Zc"], c["bg"], c["L"])
         assert np.array_equal(ck[0], c["ck"]) and bool(st[0]) == c["status"], (c["bg"], c["Zc"])
+
+
+def test_prbs_modulation_demodulation_golden():
+    """prbs / modulate / demodulate restatements == the reference's gen_nrPRBS, nrModulate,
+    nrDemodulate outputs (tests/golden/demod_golden.npz), bit for bit (float32 / complex64)."""
+    d = np.load(os.path.join(GOLD, "demod_golden.npz"))
+    for j, (cinit, N) in enumerate(d["prbs_meta"].tolist()):
+        assert np.array_equal(O.prbs(cinit, N), np.unpackbits(d[f"prbs{j}"])[:N]), (cinit, N)
+    for k, (Qm, n) in enumerate(d["meta"].tolist()):
+        bits = np.unpackbits(d[f"bits{k}"])[:n * Qm]
+        assert np.array_equal(O.modulate(bits, Qm).view(np.uint32), d[f"sym{k}"].view(np.uint32)), Qm
+        llr = O.demodulate(d[f"y{k}"], d[f"nv{k}"], Qm)
+        assert np.array_equal(llr.view(np.uint32), d[f"llr{k}"].view(np.uint32)), Qm
