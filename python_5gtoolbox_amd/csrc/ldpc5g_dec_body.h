@@ -380,14 +380,28 @@ __device__ __forceinline__ void dec_body(
             const T x1 = min1 - beta, x2 = min2 - beta;
             const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
             const T nB = alpha * (x2 > T(0) ? x2 : T(0));
-            // pass 2: Lr = sign * (k == argmin ? nB : nA), accumulated row-ascending (:126)
+            // pass 2: Lr = sign * (k == argmin ? nB : nA), accumulated row-ascending (:126).
+            // High-degree rows recompute their rotated addresses (see layered_row).
+            constexpr bool RECOMP = d > kRecompDeg;
+            uint32_t tzb2 = (uint32_t)tzb, tzbw2 = tzbw;
+            if constexpr (RECOMP) {
+                asm volatile("" : "+v"(tzb2));
+                asm volatile("" : "+v"(tzbw2));
+            }
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
                 if constexpr (j < KC) {
                     const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
                     const T r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
-                    lds_T& acc = at(ACC_B + j * CS * TS + rb[k]);
+                    int rbk;
+                    if constexpr (RECOMP) {
+                        const uint32_t S = (uint32_t)gshift(e0 + k) * GT;
+                        rbk = (int)min(tzb2 + S, tzbw2 + S);
+                    } else {
+                        rbk = rb[k];
+                    }
+                    lds_T& acc = at(ACC_B + j * CS * TS + rbk);
                     acc = acc + r;
                 }
             });

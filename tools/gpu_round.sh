@@ -58,11 +58,11 @@ if has ab; then
   echo "[gpu_round] decoder A/B builds (build/alt/*.so)"
   for lib in python_5gtoolbox_amd/libldpc5g.so build/alt/*.so; do
     n=$(basename "$lib" .so)
-    LDPC5G_LIB=$ROOT/$lib timeout -k 10 240 python -u -m pytest tests/test_gpu_ldpc.py -q -x -k "layered or packed or z384" \
+    LDPC5G_LIB=$ROOT/$lib timeout -k 10 240 python -u -m pytest tests/test_gpu_ldpc.py -q -x -k "${AB_TESTS:-layered or packed or z384}" \
         --timeout 120 --timeout-method thread > "$OUT/ab_test_$n.log" 2>&1
     rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then die "ab test $n" $rc; fi
-    LDPC5G_LIB=$ROOT/$lib timeout -k 10 120 python -u tools/probe.py layered 4096 8192 > "$OUT/ab_probe_$n.log" 2>&1 || die "ab probe $n" $?
-    echo "$n: tests $(tail -1 "$OUT/ab_test_$n.log") | $(grep layered "$OUT/ab_probe_$n.log" | tr '\n' ' ')"
+    LDPC5G_LIB=$ROOT/$lib timeout -k 10 120 python -u tools/probe.py ${AB_PROBE:-layered} 4096 16384 > "$OUT/ab_probe_$n.log" 2>&1 || die "ab probe $n" $?
+    echo "$n: tests $(tail -1 "$OUT/ab_test_$n.log") | $(grep -v amdgpu.ids "$OUT/ab_probe_$n.log" | tr '\n' ' ')"
   done
 fi
 if has pmc; then
