@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--L", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the bounded CPU-baseline sample (0 disables)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU-baseline processes (default: min(16, os.cpu_count()), the box's "
+                         "CPU share per GPU)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary measurements (early exit, flooding, encoder)")
     return ap.parse_args()
@@ -107,11 +110,13 @@ def timed(torch, dist, world, fn, steps, warmup):
     return wall, ev
 
 
-def cpu_baseline(seconds, schedule, alpha, L):
-    """Oracle (numpy restatement, one core) on a bounded sample of the same workload."""
+def _cpu_worker(job):
+    """One host process of the CPU baseline: the oracle (numpy) decoding 8-codeblock batches of
+    the headline workload until `seconds` have passed."""
+    seconds, schedule, alpha, L, seed = job
     import numpy as np
     from oracle import ldpc_oracle as O
-    rng = np.random.default_rng(11)
+    rng = np.random.default_rng(seed)
     n = 8
     ck = rng.integers(0, 2, (n, K_INFO)).astype(np.int8)
     llr = O.bpsk_awgn_llr(O.encode(ck, BG), -3.0, rng).astype(np.float32)
@@ -123,11 +128,34 @@ def cpu_baseline(seconds, schedule, alpha, L):
         done += n
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": round(done / el, 3), "unit": "codeblocks/s", "cores": 1, "kind": "port",
-            "sample": f"{done} BG1 Zc=384 codeblocks ({n} per call), {schedule} NMS alpha={alpha} "
-                      f"L={L}, snr -3 dB (all iterations), oracle/ldpc_oracle.py numpy, "
-                      f"{el:.1f} s on 1 host core",
+            return done, el
+
+
+def cpu_baseline(seconds, schedule, alpha, L, procs):
+    """Oracle (numpy restatement, kind "port") on a bounded sample of the same workload, one
+    process per host core up to `procs`.  Runs before this process touches
+    the GPU, so the spawned workers never inherit a GPU context."""
+    import multiprocessing as mp
+    import platform
+    jobs = [(seconds, schedule, alpha, L, 11 + i) for i in range(procs)]
+    if procs == 1:
+        res = [_cpu_worker(jobs[0])]
+    else:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, jobs)
+    done = sum(d for d, _ in res)
+    el = max(e for _, e in res)
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": round(done / el, 3), "unit": "codeblocks/s", "cores": procs, "kind": "port",
+            "sample": f"{done} BG1 Zc=384 codeblocks (8 per call) over {procs} processes, "
+                      f"{schedule} NMS alpha={alpha} L={L}, snr -3 dB (all iterations), "
+                      f"oracle/ldpc_oracle.py numpy, {el:.1f} s; host {cpu}, "
+                      f"os.cpu_count()={os.cpu_count()}",
             "reference_measured_in_build_container": {
                 "value": 0.073, "unit": "codeblocks/s", "cores": 1,
                 "note": "py5gphy nr_decode_ldpc itself, 13.2-14.1 s per BG1 Zc=384 CB at L=8 "
@@ -236,6 +264,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cpu_res = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:   # before any GPU initialisation
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
+            procs = 1   # a profiler may have initialised the GPU already: no spawned workers
+        cpu_res = cpu_baseline(args.cpu_seconds, args.schedule, args.alpha, args.L, procs)
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
@@ -342,10 +376,8 @@ def main():
         ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
         res["extras"] = ex
 
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.schedule, args.alpha, args.L)
-    elif rank == 0:
-        res["cpu_baseline"] = None
+    if rank == 0:
+        res["cpu_baseline"] = cpu_res
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
