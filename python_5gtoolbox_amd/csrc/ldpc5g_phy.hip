@@ -67,16 +67,37 @@ __device__ __forceinline__ uint32_t prbs_step32(uint32_t& s, bool x2) {
 }
 
 constexpr int kPrbsWordsPerThread = 8;
+constexpr int kPrbsLaneLog = 8;   // log2(32 * kPrbsWordsPerThread): bits per thread
+static_assert(32 * kPrbsWordsPerThread == 1 << kPrbsLaneLog, "bits per thread must be 2^kPrbsLaneLog");
 
-// words[t][w] = c(32w .. 32w+31) of transport block t (gen_nrPRBS(cinit[t], ...) packed)
+// T^(m 2^kPrbsLaneLog) s for m < 256: the per-thread part of the jump
+__device__ __forceinline__ uint32_t prbs_jump_lane(int q, uint32_t s, uint32_t m) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if ((m >> i) & 1u) {
+            uint32_t r = 0;
+#pragma unroll
+            for (int j = 0; j < 31; ++j) r ^= ((s >> j) & 1u) ? kPrbs.t[q][kPrbsLaneLog + i][j] : 0u;
+            s = r;
+        }
+    }
+    return s;
+}
+
+// words[t][w] = c(32w .. 32w+31) of transport block t (gen_nrPRBS(cinit[t], ...) packed).  The
+// jump to the workgroup's first bit is uniform (scalar); each thread then jumps by
+// threadIdx.x * 256 bits with at most 8 matrix products.
 __global__ __launch_bounds__(256) void prbs_kernel(const uint32_t* __restrict__ cinit, int64_t nw,
                                                    uint32_t* __restrict__ words, int64_t ldw) {
     const int t = blockIdx.y;
-    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPrbsWordsPerThread;
+    const int64_t wb = (int64_t)blockIdx.x * 256 * kPrbsWordsPerThread;
+    const int64_t w0 = wb + (int64_t)threadIdx.x * kPrbsWordsPerThread;
+    const uint32_t nb = 1600u + 32u * (uint32_t)wb;
+    uint32_t s1 = prbs_jump(0, 1u, nb);
+    uint32_t s2 = prbs_jump(1, cinit[t] & 0x7FFFFFFFu, nb);
     if (w0 >= nw) return;
-    const uint32_t n0 = 1600u + 32u * (uint32_t)w0;
-    uint32_t s1 = prbs_jump(0, 1u, n0);
-    uint32_t s2 = prbs_jump(1, cinit[t] & 0x7FFFFFFFu, n0);
+    s1 = prbs_jump_lane(0, s1, threadIdx.x);
+    s2 = prbs_jump_lane(1, s2, threadIdx.x);
     uint32_t* out = words + (int64_t)t * ldw;
 #pragma unroll
     for (int k = 0; k < kPrbsWordsPerThread; ++k) {

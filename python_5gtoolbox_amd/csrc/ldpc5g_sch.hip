@@ -11,9 +11,10 @@
 // ULSCH_decoding (nr_ulsch_decode.py:13-110).
 //
 // All of it is byte / integer work bound by HBM or latency, not arithmetic: bits stay one per
-// int8 (the reference's own representation and the encoder/decoder ABI), a wave packs 64 of them
-// with one ballot, and CRCs are combined across threads, codeblocks and transport blocks through
-// the linearity crc(M1 || M2) = crc(M1) * x^|M2| + crc(M2)  (mod g).
+// int8 (the reference's own representation and the encoder/decoder ABI); a lane reads 64 of them
+// with 16-byte loads, packs them into a word and runs a byte-table LFSR over it, and CRCs are
+// combined across lanes, codeblocks and transport blocks through the linearity
+// crc(M1 || M2) = crc(M1) * x^|M2| + crc(M2)  (mod g).
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -48,11 +49,12 @@ __host__ __device__ constexpr uint32_t crc_mulmod(uint32_t a, uint32_t b, int L,
 }
 
 constexpr int kCrcNT = 256;              // threads of a CRC workgroup
-constexpr int kCrcChunkWords = kCrcNT;   // 64-bit words per workgroup chunk (16384 bits)
+constexpr int kCrcChunkWords = kCrcNT;   // 64-bit message words per workgroup chunk (16384 bits)
 
 struct CrcTables {
     uint32_t xp2[6][40];                // x^(2^i) mod g
     uint32_t x64[6][kCrcChunkWords];    // x^(64 m) mod g
+    uint32_t byte[6][256];              // v(x) x^L mod g: the register after feeding byte v, MSB first
 };
 constexpr CrcTables make_crc_tables() {
     CrcTables t{};
@@ -63,6 +65,14 @@ constexpr CrcTables make_crc_tables() {
         for (int i = 1; i < 40; ++i) t.xp2[p][i] = crc_mulmod(t.xp2[p][i - 1], t.xp2[p][i - 1], L, g);
         t.x64[p][0] = 1u;
         for (int m = 1; m < kCrcChunkWords; ++m) t.x64[p][m] = crc_mulmod(t.x64[p][m - 1], t.xp2[p][6], L, g);
+        for (int v = 0; v < 256; ++v) {
+            uint32_t reg = 0;
+            for (int k = 7; k >= 0; --k) {
+                const uint32_t fb = ((reg >> (L - 1)) ^ (uint32_t)(v >> k)) & 1u;
+                reg = ((reg << 1) & ((1u << L) - 1u)) ^ (fb ? g : 0u);
+            }
+            t.byte[p][v] = reg;
+        }
     }
     return t;
 }
@@ -77,71 +87,169 @@ __device__ uint32_t crc_xpow(int64_t n, int p) {   // x^n mod g
     return r;
 }
 
-// CRC register of 64 message bits, bit 0 first: W(x) x^L mod g (crc.py:28-33 long division)
-__device__ __forceinline__ uint32_t crc_word64(uint64_t w, int L, uint32_t g) {
-    uint32_t reg = 0;
-    const uint32_t mask = (1u << L) - 1u;
-#pragma unroll
-    for (int b = 0; b < 64; ++b) {
-        const uint32_t fb = ((reg >> (L - 1)) ^ (uint32_t)(w >> b)) & 1u;
-        reg = ((reg << 1) & mask) ^ (fb ? g : 0u);
-    }
-    return reg;
-}
-
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
     return v;
 }
 
-// Contribution of chunk `chunk` (64-bit words [256 chunk, 256 chunk + 256)) to the CRC of an
-// nbits-long message read through bitf(i) (0/1): crc(chunk) * x^(bits after the chunk).  The
-// message is left-padded with zeros to whole words (leading zeros do not change a CRC).  Valid
-// in thread 0; every thread of the (kCrcNT-thread) workgroup must call it.
-template <typename BitF>
-__device__ uint32_t wg_crc_chunk(BitF bitf, int64_t nbits, int64_t chunk, int p, uint32_t* red) {
-    const int L = kCrcPoly[p].L;
-    const uint32_t g = kCrcPoly[p].g;
+// Per-workgroup CRC state in LDS: byte tables of the (up to two) polynomials being computed,
+// wave partials and the ragged last word's CRC.
+struct CrcLds {
+    uint32_t tab[2][256];
+    uint32_t red[2][kCrcNT / 64];
+    uint32_t part[2];
+};
+__device__ __forceinline__ void crc_lds_init(CrcLds& S, int p0, int p1) {   // kCrcNT == 256
+    S.tab[0][threadIdx.x] = kCrcTab.byte[p0][threadIdx.x];
+    if (p1 >= 0) S.tab[1][threadIdx.x] = kCrcTab.byte[p1][threadIdx.x];
+    __syncthreads();
+}
+
+// reg * x^8 + byte * x^L  (mod g): one table step, message byte MSB (= earliest bit) first
+__device__ __forceinline__ uint32_t crc_step8(uint32_t reg, uint32_t byte, int L, const uint32_t* tab) {
+    if (L >= 8) return ((reg << 8) & ((1u << L) - 1u)) ^ tab[((reg >> (L - 8)) ^ byte) & 0xFFu];
+    return tab[((reg << (8 - L)) ^ byte) & 0xFFu];
+}
+// CRC register of the nb <= 64 message bits held in w (bit k = message bit k): W(x) x^L mod g
+// (the long division of crc.py:28-33)
+__device__ __forceinline__ uint32_t crc_word(uint64_t w, int nb, int L, uint32_t g, const uint32_t* tab) {
+    const uint64_t rv = __builtin_bitreverse64(w);   // message bit k at bit 63 - k
+    uint32_t reg = 0;
+    if (nb == 64) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) reg = crc_step8(reg, (uint32_t)(rv >> (56 - 8 * b)), L, tab);
+        return reg;
+    }
+    int k = 0;
+    for (; k + 8 <= nb; k += 8) reg = crc_step8(reg, (uint32_t)(rv >> (56 - k)), L, tab);
+    for (; k < nb; ++k) {
+        const uint32_t fb = ((reg >> (L - 1)) ^ (uint32_t)(w >> k)) & 1u;
+        reg = ((reg << 1) & ((1u << L) - 1u)) ^ (fb ? g : 0u);
+    }
+    return reg;
+}
+
+// LSBs of four 0/1 bytes -> 4 bits (byte j -> bit j)
+__device__ __forceinline__ uint32_t pack4(uint32_t x) { return (((x & 0x01010101u) * 0x01020408u) >> 24) & 0xFu; }
+
+template <typename V>
+__device__ __forceinline__ uint64_t load_bits64_vec(const int8_t* p, int8_t* dst) {
+    constexpr int n = 64 / (int)sizeof(V);
+    V x[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) x[k] = reinterpret_cast<const V*>(p)[k];
+    uint64_t w = 0;
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+        const uint32_t* u = reinterpret_cast<const uint32_t*>(&x[k]);
+#pragma unroll
+        for (int j = 0; j < (int)sizeof(V) / 4; ++j)
+            w |= (uint64_t)pack4(u[j]) << (4 * (k * (int)sizeof(V) / 4 + j));
+    }
+    if (dst) {
+#pragma unroll
+        for (int k = 0; k < n; ++k) reinterpret_cast<V*>(dst)[k] = x[k];
+    }
+    return w;
+}
+// nb <= 64 message bytes at p (0/1 each) -> bits of a word (byte j -> bit j); copies the bytes to
+// dst when given.  `al` = common alignment of p and dst (16, 8, 4 or 1), uniform per workgroup.
+__device__ __forceinline__ uint64_t load_bits64(const int8_t* p, int nb, int8_t* dst, int al) {
+    if (nb == 64) {
+        if (al >= 16) return load_bits64_vec<uint4>(p, dst);
+        if (al >= 8) return load_bits64_vec<uint2>(p, dst);
+        if (al >= 4) return load_bits64_vec<uint32_t>(p, dst);
+    }
+    uint64_t w = 0;
+    for (int j = 0; j < nb; ++j) {
+        const int8_t v = p[j];
+        w |= (uint64_t)(v & 1) << j;
+        if (dst) dst[j] = v;
+    }
+    return w;
+}
+__device__ __forceinline__ int ptr_align(const void* a, const void* b) {
+    const uintptr_t u = (uintptr_t)a | (b ? (uintptr_t)b : 0);
+    return (u & 15) == 0 ? 16 : (u & 7) == 0 ? 8 : (u & 3) == 0 ? 4 : 1;
+}
+
+// Contribution of chunk `chunk` (64-bit words [256 chunk, 256 chunk + 256), word q = message bits
+// [64q, 64q + 64)) of the nbits-long message at src (one int8 0/1 per bit) to its CRC under
+// polynomial ids p[0..NP): crc(chunk) * x^(bits after the chunk), in out[] of thread 0.  Each lane
+// loads its word's 64 bytes with vector loads (copying them to dst if given), runs a byte-table
+// LFSR over them and scales the result by x^(64 (words after it in the chunk)); the workgroup XORs
+// the partials and thread 0 applies the chunk's distance to the end.  All threads must call it;
+// S.tab[i] must hold the byte table of p[i].
+template <int NP>
+__device__ void wg_crc_mem(const int8_t* src, int8_t* dst, int64_t nbits, int64_t chunk,
+                           const int (&p)[NP], CrcLds& S, uint32_t (&out)[NP]) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t nw = (nbits + 63) >> 6, pad = nw * 64 - nbits;
-    const int64_t q0 = chunk * kCrcChunkWords;
-    const int64_t qe = min(q0 + kCrcChunkWords - 1, nw - 1);   // last word of the chunk
-    uint64_t mine = 0;
-#pragma unroll 8
-    for (int k = 0; k < 64; ++k) {   // word q0 + 64 wv + k, bit `lane`: one coalesced 64-B row
-        const int64_t q = q0 + 64 * wv + k;
-        const int64_t i = q * 64 + lane - pad;
-        const bool b = q <= qe && i >= 0 && (bitf(i) & 1);
-        const uint64_t m = __builtin_amdgcn_ballot_w64(b);
-        mine = lane == k ? m : mine;
+    const int64_t nfull = nbits >> 6;
+    const int lw = (int)(nbits & 63);
+    const int64_t q0 = chunk * kCrcChunkWords, q = q0 + threadIdx.x;
+    const int64_t qf = min(q0 + kCrcChunkWords - 1, nfull - 1);   // last full word in the chunk
+    const int al = ptr_align(src, dst);
+    uint32_t c[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) c[i] = 0;
+    if (q < nfull || (q == nfull && lw > 0)) {
+        const int nb = q < nfull ? 64 : lw;
+        const uint64_t w = load_bits64(src + 64 * q, nb, dst ? dst + 64 * q : nullptr, al);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int L = kCrcPoly[p[i]].L;
+            const uint32_t g = kCrcPoly[p[i]].g;
+            const uint32_t r = crc_word(w, nb, L, g, S.tab[i]);
+            if (q < nfull) {
+                c[i] = crc_mulmod(r, kCrcTab.x64[p[i]][qf - q], L, g);
+            } else {
+                S.part[i] = r;   // ragged last word: nothing follows it
+            }
+        }
     }
-    const int64_t q = q0 + 64 * wv + lane;
-    uint32_t c = 0;
-    if (q <= qe) c = crc_mulmod(crc_word64(mine, L, g), kCrcTab.x64[p][qe - q], L, g);
-    c = wave_xor(c);
-    if (lane == 0) red[wv] = c;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        c[i] = wave_xor(c[i]);
+        if (lane == 0) S.red[i][wv] = c[i];
+    }
     __syncthreads();
-    uint32_t r = 0;
     if (threadIdx.x == 0) {
-        for (int w = 0; w < kCrcNT / 64; ++w) r ^= red[w];
-        r = crc_mulmod(r, crc_xpow(64 * (nw - 1 - qe), p), L, g);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            uint32_t r = 0;
+            for (int w = 0; w < kCrcNT / 64; ++w) r ^= S.red[i][w];
+            if (qf >= q0 && r)
+                r = crc_mulmod(r, crc_xpow(64 * (nfull - 1 - qf) + lw, p[i]), kCrcPoly[p[i]].L, kCrcPoly[p[i]].g);
+            if (lw > 0 && nfull >= q0 && nfull < q0 + kCrcChunkWords) r ^= S.part[i];
+            out[i] = r;
+        }
     }
     __syncthreads();
-    return r;
 }
 
 __host__ __device__ inline int64_t crc_chunks(int64_t nbits) {
     return ((nbits + 63) / 64 + kCrcChunkWords - 1) / kCrcChunkWords;
 }
 
+// CRC register of n <= 32 bits given MSB-first in v (bit n-1 first), continuing from reg
+__device__ __forceinline__ uint32_t crc_bits_msb(uint32_t reg, uint32_t v, int n, int L, uint32_t g) {
+    for (int k = n - 1; k >= 0; --k) {
+        const uint32_t fb = ((reg >> (L - 1)) ^ (v >> k)) & 1u;
+        reg = ((reg << 1) & ((1u << L) - 1u)) ^ (fb ? g : 0u);
+    }
+    return reg;
+}
+
 // rem[r] ^= crc contribution of chunk blockIdx.y of row r (rem zeroed by the launcher)
 __global__ __launch_bounds__(kCrcNT) void crc_rows_kernel(const int8_t* __restrict__ bits, int64_t ld,
                                                           int64_t nbits, int p, uint32_t* rem) {
-    __shared__ uint32_t red[kCrcNT / 64];
-    const int8_t* row = bits + (int64_t)blockIdx.x * ld;
-    const uint32_t c = wg_crc_chunk([&](int64_t i) { return (int)row[i]; }, nbits, blockIdx.y, p, red);
-    if (threadIdx.x == 0 && c) atomicXor(&rem[blockIdx.x], c);
+    __shared__ CrcLds S;
+    crc_lds_init(S, p, -1);
+    const int pp[1] = {p};
+    uint32_t c[1];
+    wg_crc_mem<1>(bits + (int64_t)blockIdx.x * ld, nullptr, nbits, blockIdx.y, pp, S, c);
+    if (threadIdx.x == 0 && c[0]) atomicXor(&rem[blockIdx.x], c[0]);
 }
 
 // ============================================================================ SCH geometry
@@ -156,62 +264,86 @@ __device__ __forceinline__ int cb_E(const SchDev& s, int c) { return c < s.c_swi
 __device__ __forceinline__ int64_t cb_goff(const SchDev& s, int c) {
     return (int64_t)c * s.E_lo + (int64_t)max(0, c - s.c_switch) * (s.E_hi - s.E_lo);
 }
-// dn position of the k-th bit selected from the circular buffer (k0 first, fillers skipped)
-__device__ __forceinline__ int sel_pos(const SchDev& s, int64_t k) {
-    const int idx = (int)((s.start + k) % s.size);
-    return idx < s.f0 ? idx : idx + s.Fin;
-}
 
 // ------------------------------------------------------------------------------- transmit
 // TB CRC (24A / 16) of every transport block: tbcrc[t] ^= chunk contributions
 __global__ __launch_bounds__(kCrcNT) void tb_crc_kernel(const int8_t* __restrict__ trblk, int64_t lda,
                                                         SchDev s, uint32_t* tbcrc) {
-    __shared__ uint32_t red[kCrcNT / 64];
-    const int8_t* row = trblk + (int64_t)blockIdx.x * lda;
-    const uint32_t c = wg_crc_chunk([&](int64_t i) { return (int)row[i]; }, s.A, blockIdx.y, s.tbp, red);
-    if (threadIdx.x == 0 && c) atomicXor(&tbcrc[blockIdx.x], c);
+    __shared__ CrcLds S;
+    crc_lds_init(S, s.tbp, -1);
+    const int pp[1] = {s.tbp};
+    uint32_t c[1];
+    wg_crc_mem<1>(trblk + (int64_t)blockIdx.x * lda, nullptr, s.A, blockIdx.y, pp, S, c);
+    if (threadIdx.x == 0 && c[0]) atomicXor(&tbcrc[blockIdx.x], c[0]);
 }
 
 // codeblock segmentation + CRC24B (nr_ldpc_cbsegment.py:24-32): codeblock (t, c) -> ck row
-// t*C + c: cbz bits of (TB || TB CRC), its CRC24B when C > 1, fillers -1 up to K
+// t*C + c: cbz bits of (TB || TB CRC), its CRC24B when C > 1, fillers -1 up to K.  The TB bits
+// are copied by the CRC pass itself; the TB CRC bits that end the last codeblock are folded in
+// by linearity, crc(M1 || M2) = crc(M1) x^|M2| + crc(M2).
 __global__ __launch_bounds__(kCrcNT) void cbseg_kernel(const int8_t* __restrict__ trblk, int64_t lda,
                                                        const uint32_t* __restrict__ tbcrc, SchDev s,
                                                        int8_t* __restrict__ ck) {
-    __shared__ uint32_t red[kCrcNT / 64];
+    __shared__ CrcLds S;
     __shared__ uint32_t cbcrc;
+    crc_lds_init(S, LDPC5G_CRC24B, -1);
     const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
-    const int8_t* tb = trblk + (int64_t)t * lda;
     const uint32_t tc = tbcrc[t];
     const int64_t base = (int64_t)c * s.cbz;
-    auto seg = [&](int64_t j) -> int {
-        const int64_t i = base + j;
-        return i < s.A ? (int)(tb[i] & 1) : (int)((tc >> (s.Ltb - 1 - (int)(i - s.A))) & 1u);
-    };
-    if (s.C > 1) {
-        const uint32_t v = wg_crc_chunk(seg, s.cbz, 0, LDPC5G_CRC24B, red);
-        if (threadIdx.x == 0) cbcrc = v;
-        __syncthreads();
-    }
+    const int nm = (int)min((int64_t)s.cbz, (int64_t)s.A - base);   // TB bits in this codeblock
+    const int nt = s.cbz - nm;                                       // TB CRC bits after them
     int8_t* out = ck + (int64_t)r * s.K;
-    for (int j = threadIdx.x; j < s.K; j += kCrcNT) {
-        int8_t v = -1;
-        if (j < s.cbz) v = (int8_t)seg(j);
-        else if (j < s.K_apo) v = (int8_t)((cbcrc >> (23 - (j - s.cbz))) & 1u);
-        out[j] = v;
+    const int pp[1] = {LDPC5G_CRC24B};
+    uint32_t v[1];
+    wg_crc_mem<1>(trblk + (int64_t)t * lda + base, out, nm, 0, pp, S, v);
+    if (threadIdx.x == 0) {
+        const uint32_t g = kCrcPoly[LDPC5G_CRC24B].g;
+        const uint32_t tail = nt ? tc >> (s.Ltb - nt) : 0u;
+        cbcrc = crc_mulmod(v[0], crc_xpow(nt, LDPC5G_CRC24B), 24, g) ^ crc_bits_msb(0u, tail, nt, 24, g);
+    }
+    __syncthreads();
+    const uint32_t cb = cbcrc;
+    for (int j = nm + threadIdx.x; j < s.K; j += kCrcNT) {
+        int8_t b = -1;
+        if (j < s.cbz) b = (int8_t)((tc >> (s.Ltb - 1 - (j - nm))) & 1u);
+        else if (j < s.K_apo) b = (int8_t)((cb >> (23 - (j - s.cbz))) & 1u);
+        out[j] = b;
     }
 }
 
 // rate matching (nr_ldpc_ratematch.py:64-97): bit selection from k0 skipping fillers, then the
-// Qm-row interleaver, written at the codeblock's offset in g (code block concatenation)
+// Qm-row interleaver, written at the codeblock's offset in g (code block concatenation).  One
+// thread per interleaver column i < E/Qm: it writes the Qm consecutive output bits e = i Qm + q,
+// read from the selected-bit stream at k = q E/Qm + i, so for every q a wave reads consecutive
+// bytes of dn and writes 64 Qm consecutive bytes of g.
 __global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict__ dn, SchDev s,
                                                         int8_t* __restrict__ g, int64_t ldg) {
     const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
     const int E = cb_E(s, c), EQ = E / s.Qm;
-    const int e = blockIdx.y * 256 + threadIdx.x;
-    if (e >= E) return;
-    const int q = e % s.Qm, i = e / s.Qm;
-    const int64_t k = (int64_t)q * EQ + i;
-    g[(int64_t)t * ldg + cb_goff(s, c) + e] = dn[(int64_t)r * s.N + sel_pos(s, k)];
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (i >= EQ) return;
+    const int8_t* src = dn + (int64_t)r * s.N;
+    int8_t* dst = g + (int64_t)t * ldg + cb_goff(s, c) + (int64_t)i * s.Qm;
+    const uint32_t size = (uint32_t)s.size, step = (uint32_t)(EQ % s.size);
+    uint32_t idx = (uint32_t)(((int64_t)s.start + i) % s.size);   // circular-buffer index of k = i
+    if (s.Qm == 8 && ((uintptr_t)dst & 7) == 0) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int pos = (int)idx < s.f0 ? (int)idx : (int)idx + s.Fin;
+            w |= (uint64_t)(uint8_t)src[pos] << (8 * q);
+            idx += step;
+            if (idx >= size) idx -= size;
+        }
+        *reinterpret_cast<uint64_t*>(dst) = w;
+        return;
+    }
+    for (int q = 0; q < s.Qm; ++q) {
+        const int pos = (int)idx < s.f0 ? (int)idx : (int)idx + s.Fin;
+        dst[q] = src[pos];
+        idx += step;
+        if (idx >= size) idx -= size;
+    }
 }
 
 // -------------------------------------------------------------------------------- receive
@@ -269,25 +401,32 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     }
 }
 
-// TB reassembly + checks (nr_dlsch_decode.py:93-106) for codeblock (t, c): CB CRC24B over
-// ck[0:K_apo] when C > 1 (cb_ok = remainder 0), copy of ck[0:cbz] to the TB bits, and this
-// codeblock's share of the TB CRC remainder, crc(seg) * x^((C-1-c) cbz), XORed into tbrem[t].
+// TB reassembly + checks (nr_dlsch_decode.py:93-106) for codeblock (t, c), one pass over
+// ck[0:cbz]: the TB CRC share crc(seg) * x^((C-1-c) cbz), XORed into tbrem[t]; CRC24B over
+// ck[0:K_apo] when C > 1 (cb_ok = remainder 0) as crc24B(ck[0:cbz]) x^24 + crc24B(ck[cbz:K_apo]);
+// and the copy of ck[0:cbz] to the TB bits.
 __global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restrict__ ck, int64_t ldc,
                                                           SchDev s, int8_t* __restrict__ tbblk,
                                                           int64_t ldb, uint8_t* __restrict__ cb_ok,
                                                           uint32_t* tbrem) {
-    __shared__ uint32_t red[kCrcNT / 64];
+    __shared__ CrcLds S;
+    crc_lds_init(S, s.tbp, LDPC5G_CRC24B);
     const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
     const int8_t* row = ck + (int64_t)r * ldc;
-    auto bit = [&](int64_t i) { return (int)row[i]; };
-    uint32_t cbr = 0;
-    if (s.C > 1) cbr = wg_crc_chunk(bit, s.K_apo, 0, LDPC5G_CRC24B, red);
-    uint32_t tbc = wg_crc_chunk(bit, s.cbz, 0, s.tbp, red);
-    int8_t* dst = tbblk + (int64_t)t * ldb + (int64_t)c * s.cbz;
-    for (int j = threadIdx.x; j < s.cbz; j += kCrcNT) dst[j] = row[j];
+    const int pp[2] = {s.tbp, LDPC5G_CRC24B};
+    uint32_t v[2];
+    wg_crc_mem<2>(row, tbblk + (int64_t)t * ldb + (int64_t)c * s.cbz, s.cbz, 0, pp, S, v);
     if (threadIdx.x == 0) {
+        uint32_t cbr = 0;
+        if (s.C > 1) {
+            const uint32_t g = kCrcPoly[LDPC5G_CRC24B].g;
+            uint32_t tail = 0;
+            for (int j = 0; j < 24; ++j) tail = (tail << 1) | (uint32_t)(row[s.cbz + j] & 1);
+            cbr = crc_mulmod(v[1], crc_xpow(24, LDPC5G_CRC24B), 24, g) ^ crc_bits_msb(0u, tail, 24, 24, g);
+        }
         cb_ok[r] = cbr == 0u;
-        tbc = crc_mulmod(tbc, crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp), s.Ltb, kCrcPoly[s.tbp].g);
+        const uint32_t tbc = crc_mulmod(v[0], crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp), s.Ltb,
+                                        kCrcPoly[s.tbp].g);
         if (tbc) atomicXor(&tbrem[t], tbc);
     }
 }
@@ -449,8 +588,8 @@ int ldpc5g_sch_ratematch(const int8_t* ck, const ldpc5g_sch_cfg_t* cfg, int32_t 
     const int rows = T * s.C;
     if (int rc = launch_encode(ck, dn, rows, s.bgn, s.Zc, zc_index(s.Zc), s.K, s.N, st)) return rc;
     if (s.E_hi > 0)
-        hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (s.E_hi + 255) / 256), dim3(256), 0, st, dn, s,
-                           g, ldg);
+        hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (s.E_hi / s.Qm + 255) / 256), dim3(256), 0, st, dn,
+                           s, g, ldg);
     return check_hip(hipGetLastError(), "ratematch launch");
 }
 
