@@ -123,6 +123,17 @@ constexpr int lds_rows() { return BG == 1 ? 11 : 18; }
 #define LDPC5G_RECOMP_DEG 12
 #endif
 constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
+// A/B switches (off by default; r01i, 4096 / 16384 CBs: 1.629 / 1.708 M CB/s without either,
+// 1.607 / 1.695 with BATCH_READS, 1.596 / 1.696 with OPAQUE_SW -- LDS latency is hidden by the
+// three waves per SIMD, the kernel is VALU-issue bound):
+//   LDPC5G_BATCH_READS: layered pass 1 issues all of a row's LDS reads before consuming any;
+//   LDPC5G_OPAQUE_SW:   prefetched shift words kept opaque (no scalar reload after the barrier).
+#ifndef LDPC5G_BATCH_READS
+#define LDPC5G_BATCH_READS 0
+#endif
+#ifndef LDPC5G_OPAQUE_SW
+#define LDPC5G_OPAQUE_SW 0
+#endif
 // LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
 template <bool LAYERED>
 constexpr int dec_cs() { return LAYERED ? kDecThreadsL : kDecThreads; }
@@ -426,14 +437,31 @@ __device__ __forceinline__ void dec_body(
             int rb[d];
             T min1 = FT<T>::inf(), min2 = FT<T>::inf();
             uint32_t sx = 0;
+#if LDPC5G_BATCH_READS
+            // all of the row's rotated APP reads are issued before the first one is consumed, so
+            // the row waits for LDS latency once, not once per edge (lgkmcnt counts down)
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
                 if constexpr (j < KC) {
                     rb[k] = rot(gshift(e0 + k));
+                    q[k] = at(j * CS * TS + rb[k]);
+                }
+            });
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
                     const T sel = (idxo == (uint32_t)k) ? mBs : mAs;
                     const T rold = __uint_as_float(__builtin_amdgcn_bitop3_b32(u, __float_as_uint(sel), mv, 0x6c));
+#if LDPC5G_BATCH_READS
+                    q[k] = q[k] - rold;
+#else
+                    rb[k] = rot(gshift(e0 + k));
                     q[k] = at(j * CS * TS + rb[k]) - rold;
+#endif
                 } else {
                     q[k] = xl;   // degree-1 column: q is the channel LLR itself
                 }
@@ -495,6 +523,11 @@ __device__ __forceinline__ void dec_body(
             sfor<0, group_nw<BG>(g)>([&](auto wc) {
                 constexpr int w = decltype(wc)::value;
                 nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
+#if LDPC5G_OPAQUE_SW
+                // opaque: the compiler may not re-issue the constant load after the barrier
+                // (a scalar-cache round trip at the head of every row group)
+                asm volatile("" : "+s"(nsw[w]));
+#endif
             });
         };
         // layered: the ext-column LLRs of group g are loaded from global memory at the start of

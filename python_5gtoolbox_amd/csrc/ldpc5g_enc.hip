@@ -261,8 +261,43 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
 // row-word (32 bits of one base row) is expanded and stored straight to dn as 32 (or 16) bytes,
 // and the p1..p4 recursion runs inside wave 0 with wave-level syncs (no parity bit array, no LDS
 // atomics, 4 workgroup barriers instead of 9).
+// Core-column edges of the extension rows (i >= 4), row by row: the edge list of phase 6, whose
+// row index is per lane.  Copied into LDS per workgroup (with V mod Zc and the column's X offset
+// folded in) so the row loop reads its edges from LDS, not through a chain of dependent global
+// loads per edge.
+template <int BG>
+struct ExtEdges {
+    int n = 0, maxd = 0;
+    int rs[64] = {};       // rs[i - 4] .. rs[i - 3]: core edges of row i
+    int16_t e[320] = {};   // edge ids
+    constexpr ExtEdges() {
+        using P = BGT<BG>;
+        for (int i = 4; i < P::MB; ++i) {
+            rs[i - 4] = n;
+            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k)
+                if (P::COL[k] < P::KC) e[n++] = (int16_t)k;
+            maxd = n - rs[i - 4] > maxd ? n - rs[i - 4] : maxd;
+        }
+        rs[P::MB - 4] = n;
+    }
+};
+template <int BG>
+constexpr ExtEdges<BG> kExtEdges{};
+__device__ const ExtEdges<1> kExtEdges1D = ExtEdges<1>{};   // device copies (runtime-indexed)
+__device__ const ExtEdges<2> kExtEdges2D = ExtEdges<2>{};
+template <int BG>
+__device__ __forceinline__ int ext_edge_id(int c) {
+    if constexpr (BG == 1) return kExtEdges1D.e[c];
+    else return kExtEdges2D.e[c];
+}
+template <int BG>
+__device__ __forceinline__ int ext_row_start(int r) {
+    if constexpr (BG == 1) return kExtEdges1D.rs[r];
+    else return kExtEdges2D.rs[r];
+}
+
 struct EncFastLayout {
-    int K, N, W, DW, KW, words;
+    int K, N, W, DW, KW, words, tab;
 };
 template <int BG>
 __host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
@@ -273,9 +308,24 @@ __host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
     L.W = (Zc + 31) >> 5;
     L.DW = 2 * L.W + 2;
     L.KW = (L.K + 31) >> 5;
-    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2]
-    L.words = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + 2;
+    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2] | ext edge table [n] | ext row starts [MB-3]
+    L.tab = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + 2;
+    L.words = L.tab + kExtEdges<BG>.n + (P::MB - 3);
     return L;
+}
+
+// Fill the LDS edge table of phase 6: entry c = (X word offset of the edge's column) << 16 |
+// V mod Zc; then the row starts.  All loads are independent, issued with the phase-1 loads.
+template <int BG>
+__device__ __forceinline__ void enc_fill_ext_tab(uint32_t* sm, const EncFastLayout& Ly, int zi, int t, int NT) {
+    using P = BGT<BG>;
+    constexpr ExtEdges<BG> X = kExtEdges<BG>;
+    uint32_t* tab = sm + Ly.tab;
+    for (int c = t; c < X.n; c += NT) {
+        const int e = ext_edge_id<BG>(c);
+        tab[c] = ((uint32_t)(col_d<BG>(e) * Ly.DW) << 16) | (uint32_t)shift_of<BG>(zi, e);
+    }
+    for (int r = t; r <= P::MB - 4; r += NT) tab[X.n + r] = (uint32_t)ext_row_start<BG>(r);
 }
 template <int BG>
 inline size_t enc_fast_lds_bytes(int Zc) {
@@ -354,14 +404,21 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     uint32_t* p4 = pv + 3 * W;
     uint32_t* L2 = pv + 4 * W;
     if (t < 64) {
-        for (int task = t; task < 4 * W; task += 64) {
-            int i = task / W, w = task - i * W;
-            uint32_t acc = 0;
-            for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
-                int j = col_d<BG>(e);
-                if (j < P::KB) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
-            }
-            lam[i * W + w] = acc;
+        // lambda_i = A_i c: lane w < W owns word w of all four core rows; the rows' edges are
+        // compile-time (column constant, V mod Zc a scalar load), so the 4 x 19 window reads are
+        // independent LDS loads in flight together
+        if (t < W) {
+            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+            sfor<0, 4>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                sfor<P::RS[i], P::RS[i + 1]>([&](auto ec) {
+                    constexpr int e = decltype(ec)::value;
+                    constexpr int j = P::COL[e];
+                    if constexpr (j < P::KB) acc[i] ^= window32(X + j * DW, 32 * t + shift_of<BG>(zi, e));
+                });
+            });
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lam[i * W + t] = acc[i];
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
@@ -397,18 +454,28 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     }
     enc_sync<LDSONLY>();
 
-    // ---- 6. extension parity rows, each row-word stored straight to dn
+    // ---- 6. extension parity rows, each row-word stored straight to dn.  The row is per lane;
+    //      its edges come from the LDS table (enc_fill_ext_tab), read for the longest row with
+    //      the surplus entries masked, so all of a task's loads are independent
+    constexpr int MAXD = kExtEdges<BG>.maxd;
+    const uint32_t* tab = sm + Ly.tab;
+    const uint32_t* trs = tab + kExtEdges<BG>.n;
     for (int task = t; task < (P::MB - 4) * W; task += NT) {
-        int i = 4 + task / W, w = task % W;
+        const int r = task / W, w = task - r * W;
+        const int c0 = (int)trs[r], c1 = (int)trs[r + 1];
         uint32_t acc = 0;
-        for (int e = row_start_d<BG>(i); e < row_start_d<BG>(i + 1); ++e) {
-            int j = col_d<BG>(e);
-            if (j < P::KC) acc ^= window32(X + j * DW, 32 * w + shift_of<BG>(zi, e));
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k) {
+            const bool ok = c0 + k < c1;
+            const uint32_t ent = ok ? tab[c0 + k] : 0u;
+            const uint32_t v = window32(X + (ent >> 16), 32 * w + (int)(ent & 0xffffu));
+            acc ^= ok ? v : 0u;
         }
-        store_bits(dst + S + i * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+        store_bits(dst + S + (4 + r) * Zc + 32 * w, acc, min(32, Zc - 32 * w));
     }
 }
 
+constexpr int kEncChunks = 3;   // 3 x 128 threads x 32 B >= K = 8448 (BG1 Zc=384): one round
 template <int BG, bool LDSONLY>
 __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
                                                             int8_t* __restrict__ dn, int B, int Zc,
@@ -422,12 +489,25 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     extern __shared__ __align__(16) uint32_t sm[];
     const int8_t* src = ck + (int64_t)b * ldk;
     int8_t* dst = dn + (int64_t)b * ldn;
-    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn
-    for (int wi = t; wi < Ly.KW; wi += NT) {   // K = Kb*Zc is a multiple of 32 when Zc % 16 == 0
-        int4 v[2];
-        v[0] = *(const int4*)(src + wi * 32);
-        v[1] = *(const int4*)(src + wi * 32 + 16);
-        sm[wi] = enc_pack_chunk(v, wi * 32, twoZ, dst);
+    // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn.  Up to
+    //      kEncChunks 32-B chunks per thread are loaded before any is used (one HBM round trip,
+    //      not one per chunk); the phase-6 edge table is filled meanwhile.
+    for (int w0 = t; w0 < t + Ly.KW; w0 += kEncChunks * NT) {   // K = Kb*Zc: multiple of 32 here
+        int4 v[kEncChunks][2];
+#pragma unroll
+        for (int c = 0; c < kEncChunks; ++c) {
+            const int wi = w0 + c * NT;
+            if (wi < Ly.KW) {
+                v[c][0] = *(const int4*)(src + wi * 32);
+                v[c][1] = *(const int4*)(src + wi * 32 + 16);
+            }
+        }
+        if (w0 == t) enc_fill_ext_tab<BG>(sm, Ly, zi, t, NT);   // every thread, first round
+#pragma unroll
+        for (int c = 0; c < kEncChunks; ++c) {
+            const int wi = w0 + c * NT;
+            if (wi < Ly.KW) sm[wi] = enc_pack_chunk(v[c], wi * 32, twoZ, dst);
+        }
     }
     if (t < 2) sm[Ly.KW + t] = 0;
     enc_sync<LDSONLY>();
@@ -464,6 +544,7 @@ __global__ __launch_bounds__(kEncPipeNT) void ldpc_enc_pipe_kernel(const int8_t*
         }
     };
     load(b);
+    enc_fill_ext_tab<BG>(sm, Ly, zi, t, kEncPipeNT);   // same for every codeblock (one zi)
     for (; b < B; b += gridDim.x) {
         int8_t* dst = dn + (int64_t)b * ldn;
 #pragma unroll

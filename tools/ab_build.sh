@@ -2,12 +2,12 @@
 # Build A/B variants of libldpc5g.so into build/alt/<name>.so (compile-time macro switches), for
 # one GPU call to time them side by side:  LDPC5G_LIB=build/alt/<name>.so python tools/probe.py layered 4096
 set -euo pipefail
+rm -rf build/alt
 mkdir -p build/alt
 build() {   # name, extra flags
   LDPC5G_EXTRA_FLAGS="$2" python -m python_5gtoolbox_amd.build --out "build/alt/$1.so" > "build/alt/$1.log" 2>&1 &
 }
-build wg384 "-DLDPC5G_LAYERED_THREADS=384"
-build rc8 "-DLDPC5G_RECOMP_DEG=8"
-build wg384_rc8 "-DLDPC5G_LAYERED_THREADS=384 -DLDPC5G_RECOMP_DEG=8"
+build nobatch "-DLDPC5G_BATCH_READS=0"
+build opaque_sw "-DLDPC5G_OPAQUE_SW=1"
 wait
 ls -la build/alt/*.so
