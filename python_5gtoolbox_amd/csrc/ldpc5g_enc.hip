@@ -261,43 +261,45 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
 // row-word (32 bits of one base row) is expanded and stored straight to dn as 32 (or 16) bytes,
 // and the p1..p4 recursion runs inside wave 0 with wave-level syncs (no parity bit array, no LDS
 // atomics, 4 workgroup barriers instead of 9).
-// Core-column edges of the extension rows (i >= 4), row by row: the edge list of phase 6, whose
-// row index is per lane.  Copied into LDS per workgroup (with V mod Zc and the column's X offset
-// folded in) so the row loop reads its edges from LDS, not through a chain of dependent global
-// loads per edge.
+// Core-column edges of the extension rows (i >= 4), padded to MAXD slots per row: the edge list
+// of phase 6, whose row index is per lane.  Slot (r, k) holds (column << 16 | edge id) or -1.
+// Copied into LDS per workgroup with V mod Zc and the column's X offset folded in (empty slots
+// point at a zero block), so the row loop reads its edges from LDS with no masking and no chain
+// of dependent global loads.
 template <int BG>
 struct ExtEdges {
-    int n = 0, maxd = 0;
-    int rs[64] = {};       // rs[i - 4] .. rs[i - 3]: core edges of row i
-    int16_t e[320] = {};   // edge ids
+    static constexpr int R = BGT<BG>::MB - 4;
+    int maxd = 0;
+    int32_t slot[BGT<BG>::MB * 10] = {};
     constexpr ExtEdges() {
         using P = BGT<BG>;
         for (int i = 4; i < P::MB; ++i) {
-            rs[i - 4] = n;
-            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k)
-                if (P::COL[k] < P::KC) e[n++] = (int16_t)k;
-            maxd = n - rs[i - 4] > maxd ? n - rs[i - 4] : maxd;
+            int n = 0;
+            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k) n += P::COL[k] < P::KC;
+            maxd = n > maxd ? n : maxd;
         }
-        rs[P::MB - 4] = n;
+        for (int r = 0; r < R; ++r) {
+            int n = 0;
+            for (int k = P::RS[r + 4]; k < P::RS[r + 5]; ++k)
+                if (P::COL[k] < P::KC) slot[r * maxd + n++] = (P::COL[k] << 16) | k;
+            for (; n < maxd; ++n) slot[r * maxd + n] = -1;
+        }
     }
+    constexpr int size() const { return R * maxd; }
 };
 template <int BG>
 constexpr ExtEdges<BG> kExtEdges{};
+static_assert(kExtEdges<1>.size() <= BGT<1>::MB * 10 && kExtEdges<2>.size() <= BGT<2>::MB * 10, "slots");
 __device__ const ExtEdges<1> kExtEdges1D = ExtEdges<1>{};   // device copies (runtime-indexed)
 __device__ const ExtEdges<2> kExtEdges2D = ExtEdges<2>{};
 template <int BG>
-__device__ __forceinline__ int ext_edge_id(int c) {
-    if constexpr (BG == 1) return kExtEdges1D.e[c];
-    else return kExtEdges2D.e[c];
-}
-template <int BG>
-__device__ __forceinline__ int ext_row_start(int r) {
-    if constexpr (BG == 1) return kExtEdges1D.rs[r];
-    else return kExtEdges2D.rs[r];
+__device__ __forceinline__ int ext_slot(int c) {
+    if constexpr (BG == 1) return kExtEdges1D.slot[c];
+    else return kExtEdges2D.slot[c];
 }
 
 struct EncFastLayout {
-    int K, N, W, DW, KW, words, tab;
+    int K, N, W, DW, KW, words, tab, zoff;
 };
 template <int BG>
 __host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
@@ -308,38 +310,59 @@ __host__ __device__ inline EncFastLayout enc_fast_layout(int Zc) {
     L.W = (Zc + 31) >> 5;
     L.DW = 2 * L.W + 2;
     L.KW = (L.K + 31) >> 5;
-    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2] | ext edge table [n] | ext row starts [MB-3]
+    // ib[KW+2] | X[KC*DW] | lam[4W] | pv[5W + 2] | ext edge slots [R*MAXD] | zero block [DW]
     L.tab = (L.KW + 2) + P::KC * L.DW + 4 * L.W + 5 * L.W + 2;
-    L.words = L.tab + kExtEdges<BG>.n + (P::MB - 3);
+    L.zoff = L.tab + kExtEdges<BG>.size() - (L.KW + 2);   // zero block, in words from X
+    L.words = L.tab + kExtEdges<BG>.size() + L.DW;
     return L;
 }
 
-// Fill the LDS edge table of phase 6: entry c = (X word offset of the edge's column) << 16 |
-// V mod Zc; then the row starts.  All loads are independent, issued with the phase-1 loads.
+// Fill the LDS edge slots of phase 6: bit address (from X) of the window start of slot (r, k) for
+// word 0, i.e. 32 * (column * DW) + V mod Zc, or the zero block for empty slots.
 template <int BG>
 __device__ __forceinline__ void enc_fill_ext_tab(uint32_t* sm, const EncFastLayout& Ly, int zi, int t, int NT) {
-    using P = BGT<BG>;
-    constexpr ExtEdges<BG> X = kExtEdges<BG>;
     uint32_t* tab = sm + Ly.tab;
-    for (int c = t; c < X.n; c += NT) {
-        const int e = ext_edge_id<BG>(c);
-        tab[c] = ((uint32_t)(col_d<BG>(e) * Ly.DW) << 16) | (uint32_t)shift_of<BG>(zi, e);
+    for (int c = t; c < kExtEdges<BG>.size(); c += NT) {
+        const int v = ext_slot<BG>(c);
+        tab[c] = v < 0 ? 32u * (uint32_t)Ly.zoff
+                       : 32u * (uint32_t)((v >> 16) * Ly.DW) + (uint32_t)shift_of<BG>(zi, v & 0xffff);
     }
-    for (int r = t; r <= P::MB - 4; r += NT) tab[X.n + r] = (uint32_t)ext_row_start<BG>(r);
+    for (int w = t; w < Ly.DW; w += NT) tab[kExtEdges<BG>.size() + w] = 0u;
 }
 template <int BG>
 inline size_t enc_fast_lds_bytes(int Zc) {
     return (size_t)enc_fast_layout<BG>(Zc).words * 4;
 }
 
-// 32 parity bits -> 32 int8 bytes (nbits = 32 or 16) at a 16-B aligned address
+// Bit-matrix transpose between "byte k of word q" and "bit 4q + k" orders, by four delta swaps
+// of the 5 index bits: tr84 moves bit 8k + j to bit 4j + k (k < 4, j < 8); tr84_inv undoes it.
+__device__ __forceinline__ uint32_t dswap(uint32_t x, int d, uint32_t m) {
+    const uint32_t t = ((x >> d) ^ x) & m;
+    return x ^ t ^ (t << d);
+}
+__device__ __forceinline__ uint32_t tr84(uint32_t x) {
+    x = dswap(x, 12, 0x0000f0f0u);
+    x = dswap(x, 6, 0x00cc00ccu);
+    x = dswap(x, 3, 0x0a0a0a0au);
+    return dswap(x, 1, 0x22222222u);
+}
+__device__ __forceinline__ uint32_t tr84_inv(uint32_t x) {
+    x = dswap(x, 1, 0x22222222u);
+    x = dswap(x, 3, 0x0a0a0a0au);
+    x = dswap(x, 6, 0x00cc00ccu);
+    return dswap(x, 12, 0x0000f0f0u);
+}
+
+// 32 parity bits -> 32 int8 bytes (nbits = 32 or 16) at a 16-B aligned address: byte k of
+// output word q is bit 4q + k, i.e. bit q of byte k of tr84_inv(bits)
 __device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits) {
-    uint4 a = make_uint4(expand4(bits & 15u), expand4((bits >> 4) & 15u), expand4((bits >> 8) & 15u),
-                         expand4((bits >> 12) & 15u));
+    const uint32_t u = tr84_inv(bits);
+    uint4 a = make_uint4(u & 0x01010101u, (u >> 1) & 0x01010101u, (u >> 2) & 0x01010101u,
+                         (u >> 3) & 0x01010101u);
     *(uint4*)dst = a;
     if (nbits > 16) {
-        uint4 b = make_uint4(expand4((bits >> 16) & 15u), expand4((bits >> 20) & 15u),
-                             expand4((bits >> 24) & 15u), expand4(bits >> 28));
+        uint4 b = make_uint4((u >> 4) & 0x01010101u, (u >> 5) & 0x01010101u, (u >> 6) & 0x01010101u,
+                             (u >> 7) & 0x01010101u);
         *(uint4*)(dst + 16) = b;
     }
 }
@@ -352,6 +375,12 @@ __device__ __forceinline__ uint32_t enc_pack_chunk(const int4 (&v)[2], int base,
         *(int4*)(dst + base - twoZ + 16) = v[1];
     }
     const uint32_t* d = (const uint32_t*)v;
+    // common case, every byte 0 or 1 (no fillers): OR the words with byte k of word q landing in
+    // bit 8k + q, then one transpose to bit 4q + k
+    uint32_t any = 0, u = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) any |= d[q], u |= d[q] << q;
+    if (!(any & 0xfefefefeu)) return tr84(u);
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -455,23 +484,19 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     enc_sync<LDSONLY>();
 
     // ---- 6. extension parity rows, each row-word stored straight to dn.  The row is per lane;
-    //      its edges come from the LDS table (enc_fill_ext_tab), read for the longest row with
-    //      the surplus entries masked, so all of a task's loads are independent
+    //      its MAXD edge slots come from the LDS table (enc_fill_ext_tab), empty ones reading
+    //      the zero block, so all of a task's loads are independent
     constexpr int MAXD = kExtEdges<BG>.maxd;
     const uint32_t* tab = sm + Ly.tab;
-    const uint32_t* trs = tab + kExtEdges<BG>.n;
+    const int dq = NT / W, dw = NT - dq * W;   // (r, w) of task t + NT from that of task t
+    int r = t / W, w = t - r * W;
     for (int task = t; task < (P::MB - 4) * W; task += NT) {
-        const int r = task / W, w = task - r * W;
-        const int c0 = (int)trs[r], c1 = (int)trs[r + 1];
         uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k) {
-            const bool ok = c0 + k < c1;
-            const uint32_t ent = ok ? tab[c0 + k] : 0u;
-            const uint32_t v = window32(X + (ent >> 16), 32 * w + (int)(ent & 0xffffu));
-            acc ^= ok ? v : 0u;
-        }
+        for (int k = 0; k < MAXD; ++k) acc ^= window32(X, (int)tab[r * MAXD + k] + 32 * w);
         store_bits(dst + S + (4 + r) * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+        r += dq, w += dw;
+        if (w >= W) w -= W, ++r;
     }
 }
 
