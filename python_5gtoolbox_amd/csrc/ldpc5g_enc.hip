@@ -269,27 +269,31 @@ __global__ __launch_bounds__(256) void ldpc_enc_kernel(const int8_t* __restrict_
 template <int BG>
 struct ExtEdges {
     static constexpr int R = BGT<BG>::MB - 4;
-    int maxd = 0;
-    int32_t slot[BGT<BG>::MB * 10] = {};
+    int maxa = 0, maxd = 0, c0 = 0;   // section A: rows 0..3 (info columns); C from slot c0
+    int32_t slot[BGT<BG>::MB * 12] = {};
     constexpr ExtEdges() {
         using P = BGT<BG>;
-        for (int i = 4; i < P::MB; ++i) {
+        for (int i = 0; i < P::MB; ++i) {
             int n = 0;
-            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k) n += P::COL[k] < P::KC;
-            maxd = n > maxd ? n : maxd;
+            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k) n += P::COL[k] < (i < 4 ? P::KB : P::KC);
+            if (i < 4) maxa = n > maxa ? n : maxa;
+            else maxd = n > maxd ? n : maxd;
         }
-        for (int r = 0; r < R; ++r) {
+        c0 = 4 * maxa;
+        for (int i = 0; i < P::MB; ++i) {
+            const int lim = i < 4 ? P::KB : P::KC, w = i < 4 ? maxa : maxd;
+            const int base = i < 4 ? i * maxa : c0 + (i - 4) * maxd;
             int n = 0;
-            for (int k = P::RS[r + 4]; k < P::RS[r + 5]; ++k)
-                if (P::COL[k] < P::KC) slot[r * maxd + n++] = (P::COL[k] << 16) | k;
-            for (; n < maxd; ++n) slot[r * maxd + n] = -1;
+            for (int k = P::RS[i]; k < P::RS[i + 1]; ++k)
+                if (P::COL[k] < lim) slot[base + n++] = (P::COL[k] << 16) | k;
+            for (; n < w; ++n) slot[base + n] = -1;
         }
     }
-    constexpr int size() const { return R * maxd; }
+    constexpr int size() const { return c0 + R * maxd; }
 };
 template <int BG>
 constexpr ExtEdges<BG> kExtEdges{};
-static_assert(kExtEdges<1>.size() <= BGT<1>::MB * 10 && kExtEdges<2>.size() <= BGT<2>::MB * 10, "slots");
+static_assert(kExtEdges<1>.size() <= BGT<1>::MB * 12 && kExtEdges<2>.size() <= BGT<2>::MB * 12, "slots");
 __device__ const ExtEdges<1> kExtEdges1D = ExtEdges<1>{};   // device copies (runtime-indexed)
 __device__ const ExtEdges<2> kExtEdges2D = ExtEdges<2>{};
 template <int BG>
@@ -332,6 +336,13 @@ __device__ __forceinline__ void enc_fill_ext_tab(uint32_t* sm, const EncFastLayo
 template <int BG>
 inline size_t enc_fast_lds_bytes(int Zc) {
     return (size_t)enc_fast_layout<BG>(Zc).words * 4;
+}
+
+// Word q of the periodic extension X[t] = block[t mod Zc] of the Zc-bit block at bit `base` of
+// v: a plain word copy when Zc is a multiple of 32 (q < DW = 2W + 2), else a rotated window.
+__device__ __forceinline__ uint32_t ext_word(const uint32_t* v, int base, int Zc, int W, int q) {
+    if ((Zc & 31) == 0) return v[(base >> 5) + (q < W ? q : q < 2 * W ? q - W : q - 2 * W)];
+    return fetch_rot32(v, base, Zc, mod_zc(32 * q, Zc));
 }
 
 // Bit-matrix transpose between "byte k of word q" and "bit 4q + k" orders, by four delta swaps
@@ -415,10 +426,15 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     uint32_t* lam = X + P::KC * DW;
     uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
 
-    // ---- 2. periodic extensions of the information columns
-    for (int task = t; task < P::KB * DW; task += NT) {
-        int j = task / DW, q = task - j * DW;
-        X[j * DW + q] = fetch_rot32(ib, j * Zc, Zc, mod_zc(32 * q, Zc));
+    // ---- 2. periodic extensions of the information columns (task = j * DW + q)
+    {
+        const int dj = NT / DW, dq = NT - dj * DW;
+        int j = t / DW, q = t - j * DW;
+        for (int task = t; task < P::KB * DW; task += NT) {
+            X[task] = ext_word(ib, j * Zc, Zc, W, q);
+            j += dj, q += dq;
+            if (q >= DW) q -= DW, ++j;
+        }
     }
     enc_sync<LDSONLY>();
 
@@ -433,21 +449,17 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     uint32_t* p4 = pv + 3 * W;
     uint32_t* L2 = pv + 4 * W;
     if (t < 64) {
-        // lambda_i = A_i c: lane w < W owns word w of all four core rows; the rows' edges are
-        // compile-time (column constant, V mod Zc a scalar load), so the 4 x 19 window reads are
-        // independent LDS loads in flight together
-        if (t < W) {
-            uint32_t acc[4] = {0u, 0u, 0u, 0u};
-            sfor<0, 4>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                sfor<P::RS[i], P::RS[i + 1]>([&](auto ec) {
-                    constexpr int e = decltype(ec)::value;
-                    constexpr int j = P::COL[e];
-                    if constexpr (j < P::KB) acc[i] ^= window32(X + j * DW, 32 * t + shift_of<BG>(zi, e));
-                });
-            });
+        // lambda_i = A_i c: lane t = i W + w < 4W owns word w of core row i; its edges come from
+        // section A of the LDS edge slots (empty slots read the zero block), so the window reads
+        // are independent LDS loads in flight together
+        if (t < 4 * W) {
+            constexpr int MAXA = kExtEdges<BG>.maxa;
+            const int i = t / W, w = t - i * W;
+            const uint32_t* ta = sm + Ly.tab + i * MAXA;
+            uint32_t acc = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) lam[i * W + t] = acc[i];
+            for (int k = 0; k < MAXA; ++k) acc ^= window32(X, (int)ta[k] + 32 * w);
+            lam[t] = acc;
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
@@ -475,7 +487,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     // ---- 5. extensions of the 4 core parity columns; core parity bytes straight to dn
     for (int task = t; task < 4 * DW; task += NT) {
         int k = task / DW, q = task - k * DW;
-        X[(P::KB + k) * DW + q] = fetch_rot32(pv + k * W, 0, Zc, mod_zc(32 * q, Zc));
+        X[(P::KB + k) * DW + q] = ext_word(pv + k * W, 0, Zc, W, q);
     }
     for (int task = t; task < 4 * W; task += NT) {
         int k = task / W, w = task - k * W;
@@ -493,7 +505,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     for (int task = t; task < (P::MB - 4) * W; task += NT) {
         uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k) acc ^= window32(X, (int)tab[r * MAXD + k] + 32 * w);
+        for (int k = 0; k < MAXD; ++k) acc ^= window32(X, (int)tab[kExtEdges<BG>.c0 + r * MAXD + k] + 32 * w);
         store_bits(dst + S + (4 + r) * Zc + 32 * w, acc, min(32, Zc - 32 * w));
         r += dq, w += dw;
         if (w >= W) w -= W, ++r;
