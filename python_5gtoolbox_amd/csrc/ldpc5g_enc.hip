@@ -345,6 +345,22 @@ __device__ __forceinline__ uint32_t ext_word(const uint32_t* v, int base, int Zc
     return fetch_rot32(v, base, Zc, mod_zc(32 * q, Zc));
 }
 
+// 16-B store of encoder output; LDPC5G_ENC_NT=1 (A/B build) makes it non-temporal
+#ifndef LDPC5G_ENC_NT
+#define LDPC5G_ENC_NT 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st16(int8_t* p, V v) {
+#if LDPC5G_ENC_NT
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    u4 x;
+    __builtin_memcpy(&x, &v, 16);
+    __builtin_nontemporal_store(x, (u4*)p);
+#else
+    *(V*)p = v;
+#endif
+}
+
 // Bit-matrix transpose between "byte k of word q" and "bit 4q + k" orders, by four delta swaps
 // of the 5 index bits: tr84 moves bit 8k + j to bit 4j + k (k < 4, j < 8); tr84_inv undoes it.
 __device__ __forceinline__ uint32_t dswap(uint32_t x, int d, uint32_t m) {
@@ -370,11 +386,11 @@ __device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits
     const uint32_t u = tr84_inv(bits);
     uint4 a = make_uint4(u & 0x01010101u, (u >> 1) & 0x01010101u, (u >> 2) & 0x01010101u,
                          (u >> 3) & 0x01010101u);
-    *(uint4*)dst = a;
+    st16(dst, a);
     if (nbits > 16) {
         uint4 b = make_uint4((u >> 4) & 0x01010101u, (u >> 5) & 0x01010101u, (u >> 6) & 0x01010101u,
                              (u >> 7) & 0x01010101u);
-        *(uint4*)(dst + 16) = b;
+        st16(dst + 16, b);
     }
 }
 
@@ -382,8 +398,8 @@ __device__ __forceinline__ void store_bits(int8_t* dst, uint32_t bits, int nbits
 // k >= 2Zc -> 0, nr_ldpc_encode.py:32-37) and store the systematic bytes straight to dn.
 __device__ __forceinline__ uint32_t enc_pack_chunk(const int4 (&v)[2], int base, int twoZ, int8_t* dst) {
     if (base >= twoZ) {   // 2Zc and K are multiples of 32 here
-        *(int4*)(dst + base - twoZ) = v[0];
-        *(int4*)(dst + base - twoZ + 16) = v[1];
+        st16(dst + base - twoZ, v[0]);
+        st16(dst + base - twoZ + 16, v[1]);
     }
     const uint32_t* d = (const uint32_t*)v;
     // common case, every byte 0 or 1 (no fillers): OR the words with byte k of word q landing in
