@@ -127,12 +127,17 @@ constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
 // 1.607 / 1.695 with BATCH_READS, 1.596 / 1.696 with OPAQUE_SW -- LDS latency is hidden by the
 // three waves per SIMD, the kernel is VALU-issue bound):
 //   LDPC5G_BATCH_READS: layered pass 1 issues all of a row's LDS reads before consuming any;
-//   LDPC5G_OPAQUE_SW:   prefetched shift words kept opaque (no scalar reload after the barrier).
+//   LDPC5G_OPAQUE_SW:   prefetched shift words kept opaque (no scalar reload after the barrier);
+//   LDPC5G_SPLIT_MIN=d: rows of degree >= d run two two-min chains (r01n: 1.643 / 1.702 at d = 8,
+//                       1.636 / 1.679 at d = 5 vs 1.647 / 1.700 off -- no latency to remove).
 #ifndef LDPC5G_BATCH_READS
 #define LDPC5G_BATCH_READS 0
 #endif
 #ifndef LDPC5G_OPAQUE_SW
 #define LDPC5G_OPAQUE_SW 0
+#endif
+#ifndef LDPC5G_SPLIT_MIN
+#define LDPC5G_SPLIT_MIN 0
 #endif
 // LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
 template <bool LAYERED>
@@ -436,6 +441,10 @@ __device__ __forceinline__ void dec_body(
             T q[d];
             int rb[d];
             T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            // two independent two-min chains (even / odd edges) for long rows: half the
+            // dependent min/med3 latency (LDPC5G_SPLIT_MIN = smallest degree split, 0 = never)
+            constexpr bool SPLIT = LDPC5G_SPLIT_MIN > 0 && d >= LDPC5G_SPLIT_MIN;
+            T min1b = FT<T>::inf(), min2b = FT<T>::inf();
             uint32_t sx = 0;
 #if LDPC5G_BATCH_READS
             // all of the row's rotated APP reads are issued before the first one is consumed, so
@@ -467,13 +476,22 @@ __device__ __forceinline__ void dec_body(
                 }
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
                 const T aq = fabs(q[k]);
-                min2 = FT<T>::med3(min1, min2, aq);
-                min1 = fmin(min1, aq);
+                if constexpr (SPLIT && (k & 1)) {
+                    min2b = FT<T>::med3(min1b, min2b, aq);
+                    min1b = fmin(min1b, aq);
+                } else {
+                    min2 = FT<T>::med3(min1, min2, aq);
+                    min1 = fmin(min1, aq);
+                }
                 if constexpr (k % 2 == 1)   // three-input XOR
                     sx = __builtin_amdgcn_bitop3_b32(sx, FT<T>::sbits(q[k - 1]), FT<T>::sbits(q[k]), 0x96);
                 else if constexpr (k == d - 1)
                     sx ^= FT<T>::sbits(q[k]);
             });
+            if constexpr (SPLIT) {   // merge the two chains: exact (selections only), ties kept
+                min2 = fmin(fmax(min1, min1b), fmin(min2, min2b));
+                min1 = fmin(min1, min1b);
+            }
             const T x1 = min1 - beta, x2 = min2 - beta;
             const T nAs = FT<T>::xsign(alpha * (x1 > T(0) ? x1 : T(0)), sx);
             const T nBs = FT<T>::xsign(alpha * (x2 > T(0) ? x2 : T(0)), sx);
