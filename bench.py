@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU-baseline processes (default: min(16, os.cpu_count()), the box's "
                          "CPU share per GPU)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse the "
+                         "multi-rank control flow with several ranks on one GPU)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary measurements (early exit, flooding, encoder)")
     return ap.parse_args()
@@ -104,7 +107,8 @@ def timed(torch, dist, world, fn, steps, warmup):
     wall = time.perf_counter() - t0
     ev = e0.elapsed_time(e1) / 1e3
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     return wall, ev
@@ -272,10 +276,14 @@ def main():
         cpu_res = cpu_baseline(args.cpu_seconds, args.schedule, args.alpha, args.L, procs)
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))   # one rank per GPU (several only to rehearse)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from python_5gtoolbox_amd import _lib, nr_ldpc_decode as D, nr_ldpc_encode as E
     _lib.lib()
 
