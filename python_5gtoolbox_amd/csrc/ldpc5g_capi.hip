@@ -78,7 +78,7 @@ int ldpc5g_encode(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t 
     const int zi = zc_index(Zc);
     if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
     const int K = (bgn == 1 ? 22 : 10) * Zc, N = (bgn == 1 ? 66 : 50) * Zc;
-    if (B < 0 || ldk < K || ldn < N) return fail(LDPC5G_ESIZE, "bad sizes B=%d ldk=%lld ldn=%lld (K=%d N=%d)", B, (long long)ldk, (long long)ldn, K, N);
+    if (B < 0 || (B > 1 && (ldk < K || ldn < N))) return fail(LDPC5G_ESIZE, "bad sizes B=%d ldk=%lld ldn=%lld (K=%d N=%d)", B, (long long)ldk, (long long)ldn, K, N);
     if (B == 0) return LDPC5G_OK;
     if (!ck || !dn) return fail(LDPC5G_ESIZE, "null buffer");
     return launch_encode(ck, dn, B, bgn, Zc, zi, ldk, ldn, (hipStream_t)stream);
@@ -94,7 +94,7 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
     if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
     const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
     const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
-    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+    if (B < 0 || L < 0 || (B > 1 && (ldl < N || ldc < Nf)))
         return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
     if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
     if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
@@ -115,7 +115,7 @@ int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
     if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
     const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
     const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
-    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+    if (B < 0 || L < 0 || (B > 1 && (ldl < N || ldc < Nf)))
         return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
     if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
     if (B == 0) return LDPC5G_OK;
@@ -138,7 +138,7 @@ int ldpc5g_decode_bp(const double* llr, int8_t* ck, uint8_t* status, int32_t* it
     if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
     const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
     const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
-    if (B < 0 || L < 0 || ldl < N || ldc < Nf)
+    if (B < 0 || L < 0 || (B > 1 && (ldl < N || ldc < Nf)))
         return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d ldl=%lld ldc=%lld (N=%d Nf=%d)", B, L, (long long)ldl, (long long)ldc, N, Nf);
     if (scratch_elems < ldpc5g_bp_scratch_elems(B, bgn, Zc))
         return fail(LDPC5G_ESIZE, "scratch too small: %lld < %lld", (long long)scratch_elems, (long long)ldpc5g_bp_scratch_elems(B, bgn, Zc));
