@@ -54,6 +54,22 @@ template <int OP> __global__ void kern(float* out, uint32_t sv) {
       if constexpr (OP == 40) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
       if constexpr (OP == 41) asm volatile("v_ldexp_f32 %0, %0, %2" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) );
       if constexpr (OP == 42) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(p[i]) : "v"(p[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 44) asm volatile("v_ashrrev_i32 %0, 31, %0" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 45) asm volatile("v_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) : "vcc");
+      if constexpr (OP == 46) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 47) asm volatile("v_sub_f32_e64 %0, |%0|, %1" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 48) asm volatile("v_lshrrev_b32 %0, 5, %0" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 49) asm volatile("v_bfe_i32 %0, %0, 7, 1" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 50) asm volatile("v_cmp_class_f32 vcc, %0, %1" : "+v"(a[i]) : "v"(u[(i+1)&7]), "s"(sv) : "vcc");
+      if constexpr (OP == 51) asm volatile("v_min_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 52) asm volatile("v_add_u32 %0, %2, %0" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 53) asm volatile("v_mov_b32 %0, %2" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 54) asm volatile("v_sub_f32 %0, %0, %1 ; sub-abs\n v_max_f32 %0, |%0|, %1" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 55) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 56) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(u[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 57) asm volatile("v_cmp_gt_f32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "vcc");
+      if constexpr (OP == 58) asm volatile("v_cmp_gt_f32_e64 s[20:21], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "s20", "s21");
+      if constexpr (OP == 59) asm volatile("v_cmp_gt_f32_e64 s[20:21], %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "s20", "s21");
       if constexpr (OP == 43) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(p[i]) : "v"(p[(i+1)&7]), "s"(sv) );
     }
   }
@@ -108,6 +124,21 @@ int main() { float* out; hipMalloc(&out, 256 * 1024 * sizeof(float));
   run<36>("v_bfe_u32", out);
   run<37>("v_perm_b32", out);
   run<38>("v_max3_f32", out);
+  run<55>("v_cndmask_e64_vcc", out);
+  run<56>("v_cndmask_vcc_noclob", out);
+  run<57>("cmp+cndmask_vcc", out);
+  run<58>("cmp+cndmask_e64_s", out);
+  run<59>("cmp_s+cndmask_vcc", out);
+  run<44>("v_ashrrev_i32_c31", out);
+  run<45>("v_addc_co_u32_vcc", out);
+  run<46>("v_mad_u32_u24", out);
+  run<47>("v_sub_f32_abs_e64", out);
+  run<48>("v_lshrrev_b32_c5", out);
+  run<49>("v_bfe_i32_c", out);
+  run<50>("v_cmp_class_f32", out);
+  run<51>("v_min_u32_vv", out);
+  run<52>("v_add_u32_sv", out);
+  run<53>("v_mov_b32_s", out);
   run<39>("v_cvt_f32_u32", out);
   run<40>("v_xor_b32_sdwa", out);
   run<41>("v_ldexp_f32", out);
