@@ -50,6 +50,34 @@ def pmc_traffic(kernel, corrected16=False):
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12        # 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T/s
 
 
+def pmc_valu_insts(kernel):
+    """VALU wave-instructions per launch of `kernel` (4096-codeblock batch) from the committed PMC
+    summary (SQ_INSTS_VALU), or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            return float(json.load(f)["kernels"][kernel]["SQ_INSTS_VALU"])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
+def valu_block(edge_rate, launch_s, kernel, B):
+    """The decoder's binding resource: VALU issue.  Measured lane-ops/s = SQ_INSTS_VALU per launch
+    (committed PMC summary of the same kernel) x 64 lanes / this run's launch time, against the
+    full-rate peak (every lane of every SIMD32 issuing each cycle; min/max/med3, compares and
+    SGPR-operand ops issue at half that rate, tools/microbench/valu_rates.hip)."""
+    v = {"edge_updates_per_s": round(edge_rate / 1e12, 4), "unit": "T edge-updates/s",
+         "peak_lane_ops": round(VALU_PEAK_TLANE, 1),
+         "lane_ops_per_edge_update_at_peak": round(VALU_PEAK_TLANE * 1e12 / edge_rate, 2)}
+    insts = pmc_valu_insts(kernel) if B == 4096 else None
+    if insts:
+        lane_ops = insts * 64 / launch_s / 1e12
+        v.update({"measured_lane_ops": round(lane_ops, 2), "measured_unit": "T lane-op/s",
+                  "frac_of_full_rate_peak": round(lane_ops / VALU_PEAK_TLANE, 4),
+                  "valu_insts_per_edge_update": round(insts * 64 / (edge_rate * launch_s), 2),
+                  "source": "SQ_INSTS_VALU per launch, profiles/pmc_latest.json"})
+    return v
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -335,9 +363,7 @@ def main():
                      "algorithmic_bytes_per_cb": DEC_BYTES_PER_CB,
                      "launch_ms": round(launch_s * 1e3, 4),
                      "note": "decode is VALU/LDS-bound (~99 lane-op/B); see valu"},
-        "valu": {"edge_updates_per_s": round(edge_rate / 1e12, 4), "unit": "T edge-updates/s",
-                 "peak_lane_ops": round(VALU_PEAK_TLANE, 1),
-                 "lane_ops_per_edge_update_at_peak": round(VALU_PEAK_TLANE * 1e12 / edge_rate, 2)},
+        "valu": valu_block(edge_rate, launch_s, DEC_KERNEL[args.schedule], B),
     }
 
     if not args.no_extras:
@@ -361,6 +387,20 @@ def main():
         ex[f"{other}_f32_snr{args.snr:g}dB"] = {
             "codeblocks_per_s": round(B * world * max(3, args.steps // 2) / w2, 1),
             "mean_iterations": round(out[2].float().mean().item(), 3)}
+        # the reference-parity mode: float64 flooding, bit-identical to nr_decode_ldpc (what the
+        # drop-in per-codeblock API and DLSCHDecode run by default)
+        llr64 = llr.double()
+
+        def step2b():
+            D.nr_decode_ldpc_batch(llr64, ZC, BG, args.L, "min-sum", args.alpha, 0.0, "flooding",
+                                   out=out)
+        n2b = max(3, args.steps // 4)
+        w2b, _ = timed(torch, dist, world, step2b, n2b, 1)
+        ex[f"flooding_f64_snr{args.snr:g}dB"] = {
+            "codeblocks_per_s": round(B * world * n2b / w2b, 1),
+            "mean_iterations": round(out[2].float().mean().item(), 3),
+            "note": "float64 flooding = the reference's algorithm and arithmetic, bit-exact"}
+        del llr64
         # BASELINE config 2: encode-only
         dnb = torch.empty((B, N_TX), dtype=torch.int8, device=dev)
 
