@@ -130,6 +130,9 @@ constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
 //   LDPC5G_OPAQUE_SW:   prefetched shift words kept opaque (no scalar reload after the barrier);
 //   LDPC5G_SPLIT_MIN=d: rows of degree >= d run two two-min chains (r01n: 1.643 / 1.702 at d = 8,
 //                       1.636 / 1.679 at d = 5 vs 1.647 / 1.700 off -- no latency to remove).
+// Also measured and dropped (r01u): stop-rule flags double-buffered by iteration parity, so an
+// iteration without a convergence candidate ends with 2 barriers instead of 4 (1.600 / 1.701 vs
+// 1.638 / 1.711 M CB/s) -- barrier count is not what binds.
 #ifndef LDPC5G_BATCH_READS
 #define LDPC5G_BATCH_READS 0
 #endif

@@ -376,6 +376,7 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     for (int w = 1; w < kRrNT / 64; ++w) m = fmax(m, red[w]);
     const double mx = m * 10.0;
     const int64_t row = (int64_t)r * s.N;
+    const int qE = E / s.size, rE = E - qE * s.size;   // visits of rank rr: qE + (rr < rE)
     for (int p = threadIdx.x; p < s.N; p += kRrNT) {
         double v = 0.0;
         if (p >= s.f0 && p < s.f0 + s.F) {
@@ -384,13 +385,13 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
             int rr = (p < s.f0 ? p : p - s.Fin) - s.start;
             if (rr < 0) rr += s.size;
             if (rr < E) {
-                const int cnt = (E - 1 - rr) / s.size + 1;
+                const int cnt = qE + (rr < rE ? 1 : 0);   // = (E - 1 - rr) / size + 1
                 double acc = 0.0;
                 for (int j = 0; j < cnt; ++j) {
                     const int k = rr + j * s.size;
                     acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
                 }
-                v = acc / (double)cnt;
+                v = cnt == 1 ? acc : acc / (double)cnt;   // x / 1.0 == x: skip the f64 divide
             }
         }
         if (harq) {

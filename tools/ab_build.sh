@@ -7,8 +7,6 @@ mkdir -p build/alt
 build() {   # name, extra flags
   LDPC5G_EXTRA_FLAGS="$2" python -m python_5gtoolbox_amd.build --out "build/alt/$1.so" > "build/alt/$1.log" 2>&1 &
 }
-build split8 "-DLDPC5G_SPLIT_MIN=8"
-build split13 "-DLDPC5G_SPLIT_MIN=13"
-build split5 "-DLDPC5G_SPLIT_MIN=5"
+build rr_direct "-DLDPC5G_RR_LDS=0"
 wait
 ls -la build/alt/*.so
