@@ -36,11 +36,18 @@ fi
 if has trace; then
   echo "[gpu_round] rocprof kernel trace"
   cd /tmp
+  # headline only (--no-extras): the decoder's average in this summary is the bench's launch time
+  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_headline" -o run -- \
+      python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 --no-extras > "$OUT/bench_headline_under_rocprof.json" \
+      2> "$OUT/rocprof_headline.err" || { tail -20 "$OUT/rocprof_headline.err"; die trace $?; }
+  # everything (extras: encoder, flooding, config 4 / 5 chains): per-kernel table
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
       || { tail -20 "$OUT/rocprof.err"; die trace $?; }
   cd "$ROOT"
+  python tools/rocpd_summary.py "$OUT/prof_headline" > "$OUT/kernel_stats_headline.csv"
   python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
+  cut -c1-150 "$OUT/kernel_stats_headline.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
 fi
 if has probe; then
