@@ -132,7 +132,9 @@ constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
 //                       1.636 / 1.679 at d = 5 vs 1.647 / 1.700 off -- no latency to remove).
 // Also measured and dropped (r01u): stop-rule flags double-buffered by iteration parity, so an
 // iteration without a convergence candidate ends with 2 barriers instead of 4 (1.600 / 1.701 vs
-// 1.638 / 1.711 M CB/s) -- barrier count is not what binds.
+// 1.638 / 1.711 M CB/s) -- barrier count is not what binds.  Scheduler flags (r01w):
+// -amdgpu-sched-strategy=max-ilp 1.566 / 1.629, -amdgpu-schedule-metric-bias=0 1.621 / 1.702 vs
+// 1.589 / 1.696 default (run-to-run noise ~2 %).
 #ifndef LDPC5G_BATCH_READS
 #define LDPC5G_BATCH_READS 0
 #endif
