@@ -349,6 +349,9 @@ __device__ __forceinline__ uint32_t ext_word(const uint32_t* v, int base, int Zc
 #ifndef LDPC5G_ENC_NT
 #define LDPC5G_ENC_NT 0
 #endif
+#ifndef LDPC5G_ENC_COAL
+#define LDPC5G_ENC_COAL 1   // lane-contiguous 16-B pieces for the info loads / stores (A/B switch)
+#endif
 template <typename V>
 __device__ __forceinline__ void st16(int8_t* p, V v) {
 #if LDPC5G_ENC_NT
@@ -420,6 +423,36 @@ __device__ __forceinline__ uint32_t enc_pack_chunk(const int4 (&v)[2], int base,
         bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
     }
     return bits;
+}
+
+// Half-chunk variant (coalesced phase 1): 16 bytes = words q = 4h..4h+3 of a 32-byte chunk at
+// byte `base` (= chunk start + 16h); returns their bits at 16h..16h+15 (zero elsewhere), stores
+// the systematic bytes.  Same filler rule as enc_pack_chunk.
+__device__ __forceinline__ uint32_t enc_pack_half(const int4& v, int base, int h, int twoZ, int8_t* dst) {
+    if (base >= twoZ) st16(dst + base - twoZ, v);
+    const uint32_t* d = (const uint32_t*)&v;
+    uint32_t any = 0, u = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) any |= d[q], u |= d[q] << q;
+    if (!(any & 0xfefefefeu)) return tr84(u << (4 * h));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = d[q];
+        uint32_t lsb = x & 0x01010101u;
+        const uint32_t ff = (x & (x >> 1) & (x >> 2) & (x >> 3) & (x >> 4) & (x >> 5) &
+                             (x >> 6) & (x >> 7)) & 0x01010101u;
+        if (base + 4 * q >= twoZ) lsb &= ~ff;
+        bits |= ((lsb | (lsb >> 7) | (lsb >> 14) | (lsb >> 21)) & 15u) << (4 * q);
+    }
+    return bits << (16 * h);
+}
+
+// 16 parity bits (bits 0..15 of b) -> 16 int8 bytes at a 16-B aligned address
+__device__ __forceinline__ void store_bits16(int8_t* dst, uint32_t b) {
+    const uint32_t u = tr84_inv(b & 0xffffu);
+    st16(dst, make_uint4(u & 0x01010101u, (u >> 1) & 0x01010101u, (u >> 2) & 0x01010101u,
+                         (u >> 3) & 0x01010101u));
 }
 
 template <bool LDSONLY>
@@ -518,17 +551,38 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     const uint32_t* tab = sm + Ly.tab;
     const int dq = NT / W, dw = NT - dq * W;   // (r, w) of task t + NT from that of task t
     int r = t / W, w = t - r * W;
-    for (int task = t; task < (P::MB - 4) * W; task += NT) {
+    const int ntask = (P::MB - 4) * W;
+    // Zc % 32 == 0: the extension rows are one contiguous byte range and task T is its bytes
+    // [32T, 32T + 32), so a wave's 64 tasks are 2 KB in a row.  Lane l then stores 16-byte piece l
+    // and piece 64 + l of that range (words l/2 and 32 + l/2, fetched with two lane permutes):
+    // each store instruction writes 1 KB contiguous instead of 16 B every 32 B.
+    const bool coal = LDPC5G_ENC_COAL && (Zc & 31) == 0 && (NT & 63) == 0;
+    const int lane = t & 63;
+    int8_t* ext = dst + S + 4 * Zc;
+    for (int task0 = t; task0 - lane < ntask; task0 += NT) {   // wave-uniform trip count
+        const int task = task0;
         uint32_t acc = 0;
+        if (task < ntask) {
 #pragma unroll
-        for (int k = 0; k < MAXD; ++k) acc ^= window32(X, (int)tab[kExtEdges<BG>.c0 + r * MAXD + k] + 32 * w);
-        store_bits(dst + S + (4 + r) * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+            for (int k = 0; k < MAXD; ++k) acc ^= window32(X, (int)tab[kExtEdges<BG>.c0 + r * MAXD + k] + 32 * w);
+        }
+        if (coal) {
+            const int wbase = task - lane;   // first task of this wave's 64
+            const uint32_t a0 = (uint32_t)__shfl((int)acc, lane >> 1, 64);
+            const uint32_t a1 = (uint32_t)__shfl((int)acc, 32 + (lane >> 1), 64);
+            const int h = lane & 1;
+            if (wbase + (lane >> 1) < ntask) store_bits16(ext + 32 * wbase + 16 * lane, a0 >> (16 * h));
+            if (wbase + 32 + (lane >> 1) < ntask) store_bits16(ext + 32 * wbase + 1024 + 16 * lane, a1 >> (16 * h));
+        } else if (task < ntask) {
+            store_bits(dst + S + (4 + r) * Zc + 32 * w, acc, min(32, Zc - 32 * w));
+        }
         r += dq, w += dw;
         if (w >= W) w -= W, ++r;
     }
 }
 
 constexpr int kEncChunks = 3;   // 3 x 128 threads x 32 B >= K = 8448 (BG1 Zc=384): one round
+constexpr int kEncPieces = 6;   // 6 x 128 threads x 16 B >= K: one round (coalesced phase 1)
 template <int BG, bool LDSONLY>
 __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __restrict__ ck,
                                                             int8_t* __restrict__ dn, int B, int Zc,
@@ -545,6 +599,30 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn.  Up to
     //      kEncChunks 32-B chunks per thread are loaded before any is used (one HBM round trip,
     //      not one per chunk); the phase-6 edge table is filled meanwhile.
+    if (LDPC5G_ENC_COAL && (NT & 63) == 0) {
+        // 16-byte pieces, lane-contiguous (piece p = half p & 1 of chunk p / 2): every load and
+        // systematic store instruction moves 1 KB contiguous; the two halves of a chunk sit in
+        // lanes l, l ^ 1 of the same wave and are joined with one lane exchange.
+        const int np = 2 * Ly.KW;
+        // wave-uniform trip count, at least one round (the edge-table fill is in it)
+        for (int p0 = t; p0 == t || p0 - (t & 63) < np; p0 += kEncPieces * NT) {
+            int4 v[kEncPieces];
+#pragma unroll
+            for (int c = 0; c < kEncPieces; ++c) {
+                const int pc = p0 + c * NT;
+                if (pc < np) v[c] = *(const int4*)(src + 16 * pc);
+            }
+            if (p0 == t) enc_fill_ext_tab<BG>(sm, Ly, zi, t, NT);   // every thread, first round
+#pragma unroll
+            for (int c = 0; c < kEncPieces; ++c) {
+                const int pc = p0 + c * NT;
+                if (pc - (t & 63) >= np) break;   // wave-uniform
+                uint32_t part = pc < np ? enc_pack_half(v[c], 16 * pc, pc & 1, twoZ, dst) : 0u;
+                part |= (uint32_t)__shfl_xor((int)part, 1, 64);
+                if (pc < np && !(pc & 1)) sm[pc >> 1] = part;
+            }
+        }
+    } else
     for (int w0 = t; w0 < t + Ly.KW; w0 += kEncChunks * NT) {   // K = Kb*Zc: multiple of 32 here
         int4 v[kEncChunks][2];
 #pragma unroll
