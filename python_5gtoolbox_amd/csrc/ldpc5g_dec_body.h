@@ -185,7 +185,9 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int BG, typename T, bool LAYERED>
+// OFS = false: the caller guarantees beta == 0 (plain / normalized min-sum), so the offset and
+// its clamp at 0 are compiled out (min >= +0 already; the result is identical).
+template <int BG, typename T, bool LAYERED, bool OFS = true>
 __device__ __forceinline__ void dec_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -497,9 +499,13 @@ __device__ __forceinline__ void dec_body(
                 min2 = fmin(fmax(min1, min1b), fmin(min2, min2b));
                 min1 = fmin(min1, min1b);
             }
-            const T x1 = min1 - beta, x2 = min2 - beta;
-            const T nAs = FT<T>::xsign(alpha * (x1 > T(0) ? x1 : T(0)), sx);
-            const T nBs = FT<T>::xsign(alpha * (x2 > T(0) ? x2 : T(0)), sx);
+            T x1 = min1, x2 = min2;
+            if constexpr (OFS) {
+                x1 = min1 - beta, x2 = min2 - beta;
+                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const T nAs = FT<T>::xsign(alpha * x1, sx);
+            const T nBs = FT<T>::xsign(alpha * x2, sx);
             uint32_t negs = 0, idxn = 0;
             // High-degree rows (BG1 rows 0-3, d = 19): keeping all d rotated addresses live from
             // pass 1 to pass 2 beside the d messages overflows the 168-VGPR budget (scratch spills
@@ -716,14 +722,14 @@ __global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(LDPC5G_DEC_PARAMS
     dec_body<BG, T, LAYERED>(LDPC5G_DEC_ARGS);
 }
 // layered float32: 768 threads = 12 waves = 3 per SIMD (<= 168 VGPRs), G = floor(768/Zc) CBs
-template <int BG, typename T, bool LAYERED>
+template <int BG, typename T, bool LAYERED, bool OFS>
 __global__ __launch_bounds__(kDecThreadsL) __attribute__((amdgpu_waves_per_eu(3))) void
 ldpc_dec_kernel_l(LDPC5G_DEC_PARAMS) {
-    dec_body<BG, T, LAYERED>(LDPC5G_DEC_ARGS);
+    dec_body<BG, T, LAYERED, OFS>(LDPC5G_DEC_ARGS);
 }
-template <int BG, typename T, bool LAYERED>
+template <int BG, typename T, bool LAYERED, bool OFS = true>
 constexpr auto dec_kernel() {
-    if constexpr (LAYERED) return ldpc_dec_kernel_l<BG, T, LAYERED>;
+    if constexpr (LAYERED) return ldpc_dec_kernel_l<BG, T, LAYERED, OFS>;
     else return ldpc_dec_kernel<BG, T, LAYERED>;
 }
 
@@ -736,7 +742,7 @@ size_t dec_lds_bytes() {
 template <int BG, typename T, bool LAYERED>
 int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                  int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
-    auto kern = dec_kernel<BG, T, LAYERED>();
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
     const int G = dec_G(Zc, LAYERED);
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     const int threads = ((G * Zc + 63) / 64) * 64;
@@ -752,7 +758,7 @@ template <int BG, typename T, bool LAYERED>
 int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
                        const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                        int pc, hipStream_t st) {
-    auto kern = dec_kernel<BG, T, LAYERED>();
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(dec_cs<LAYERED>()), lds, st, llr, ck, status, iters, 0, 0,
