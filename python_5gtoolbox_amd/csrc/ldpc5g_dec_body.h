@@ -230,11 +230,15 @@ __device__ __forceinline__ void dec_body(
             crow = ck + r.ck_off;
             out = r.out;
         } else {
-            int cb = blockIdx.x * G + cbl;
+            // slots past the end of the batch keep lrow = llr (row 0 of CB 0): the ext-LLR
+            // prefetch below is issued by every thread and must stay inside the caller's buffer
+            const int cb = blockIdx.x * G + cbl;
             valid = cb < B;
-            lrow = llr + (int64_t)cb * ldl;
-            crow = ck + (int64_t)cb * ldc;
-            out = cb;
+            if (valid) {
+                lrow = llr + (int64_t)cb * ldl;
+                crow = ck + (int64_t)cb * ldc;
+                out = cb;
+            }
         }
     }
     const int cl = valid ? cbl : 0;
