@@ -427,10 +427,148 @@ def gen_demod():
     print("demod cases", len(meta), "prbs cases", len(prbs))
 
 
+def gen_demod2():
+    """The remaining modulations of nrModulate / nrDemodulate: BPSK, pi/2-BPSK, 1024QAM
+    (common/nrModulation.py:15-21,38-42; demodulation/demod_bpsk.py, demod_pi2_bpsk.py,
+    demod_1024qam.py), and all seven with complex64 input symbols (numpy >= 2 evaluates the
+    per-symbol formulas in float32 then; complex128 input keeps them in float64)."""
+    from py5gphy.common import nrModulation
+    from py5gphy.demodulation import nr_Demodulation
+    rng = np.random.default_rng(29)
+    mods = [("bpsk", 1, 2), ("pi/2-bpsk", 1, 2), ("qpsk", 2, 2), ("16qam", 4, 10),
+            ("64qam", 6, 42), ("256qam", 8, 170), ("1024qam", 10, 682)]
+    blobs, meta = {}, []
+    for k, (mod, Qm, scale) in enumerate(mods):
+        n = 3001 if Qm == 1 else 3000      # odd length: pi/2-BPSK's odd/even split
+        bits = rng.integers(0, 2, n * Qm)
+        sym = nrModulation.nrModulate(bits, mod)
+        A = 1 / np.sqrt(scale)
+        lev = int(np.sqrt(scale * 2)) if Qm > 1 else 2
+        y = sym.astype(np.complex128) + (rng.normal(0, 0.3, n) + 1j * rng.normal(0, 0.3, n)) * A * 3
+        th = rng.integers(-2 * lev, 2 * lev + 1, 400) * A     # exact decision thresholds
+        y[:400] = th + 1j * th[::-1]
+        y[400:410] = 0.0
+        nv = rng.uniform(0.01, 1.0, n)
+        _, llr = nr_Demodulation.nrDemodulate(y, mod, nv)
+        y64 = y.astype(np.complex64)
+        _, llr64 = nr_Demodulation.nrDemodulate(y64, mod, nv)
+        blobs[f"bits{k}"] = np.packbits(bits.astype(np.uint8))
+        blobs[f"sym{k}"] = np.asarray(sym)
+        blobs[f"y{k}"] = y
+        blobs[f"nv{k}"] = nv.astype(np.float32)
+        blobs[f"llr{k}"] = np.asarray(llr)                  # float64 for BPSK (demod_bpsk.py:9)
+        blobs[f"llr_c64_{k}"] = np.asarray(llr64)
+        meta.append((k, Qm, n))
+    np.savez_compressed(os.path.join(OUT, "demod2_golden.npz"), meta=np.array(meta, np.int64),
+                        mods=np.array([m[0] for m in mods]), **blobs)
+    print("demod2 cases", len(meta))
+
+
+def gen_config1():
+    """BASELINE config 1 exactly: BG2 Zc=8, CRC24A, for_test_5g_ldpc_encoder (nr_ldpc_decode.py:
+    229-260, global numpy RNG seeded per case) then nr_decode_ldpc(..., L=8, 'min-sum', 0.75, 0)
+    (NMS alpha=.75), 7 SNRs x 6 codeblocks."""
+    _, dec = _ref()
+    rows = []
+    blk_l, dn_l, llr_l, ck_l = [], [], [], []
+    for snr in (-3.0, -2.0, -1.0, 0.0, 1.0, 2.0, 3.0):
+        for j in range(6):
+            seed = 1000 + len(rows)
+            np.random.seed(seed)
+            blk, dn, llr = dec.for_test_5g_ldpc_encoder(8, 2, snr, "24A")
+            _, ck, status = dec.nr_decode_ldpc(llr, 8, 2, 8, "min-sum", 0.75, 0)
+            rows.append((seed, snr, int(bool(status))))
+            blk_l.append(np.asarray(blk, np.int8))
+            dn_l.append(np.asarray(dn, np.int8))
+            llr_l.append(np.asarray(llr, np.float64))
+            ck_l.append(np.asarray(ck, np.int8))
+    np.savez_compressed(os.path.join(OUT, "config1_golden.npz"),
+                        seed=np.array([r[0] for r in rows], np.int64),
+                        snr=np.array([r[1] for r in rows], np.float64),
+                        status=np.array([r[2] for r in rows], np.uint8),
+                        blk=np.stack(blk_l), dn=np.stack(dn_l), llr=np.stack(llr_l),
+                        ck=np.stack(ck_l))
+    print("config1 cases", len(rows), "converged", sum(r[2] for r in rows))
+
+
+class _NoGlobals(__import__("pickle").Unpickler):
+    """Loads plain containers only: any class or function reference in the stream raises, so
+    nothing from the file can execute."""
+    def find_class(self, module, name):
+        raise __import__("pickle").UnpicklingError(f"blocked {module}.{name}")
+
+
+# BLER pickles written by scripts/internal/sim_ldpc_internal.py:89-91 ([sim_config, labels,
+# bler_lists]) and the SNR lists of the scripts that wrote them (the pickles do not store them).
+# Left out: ldpc_decode_result_all.pickle and ldpc_decode_result_BF.pickle, whose BLER values are
+# not multiples of the current stopping rule's trial counts (an older harness made them).
+PIN_FILES = (
+    [(f"NMS_search_alpha_ZC{z}_bgn{b}.pickle", "scripts/NMS_ldpc_search_best_alpha.py:13-27", [-0.5])
+     for z in (8, 12, 28, 40, 72, 176, 208, 384) for b in (1, 2) if (z, b) != (384, 2)] +
+    [(f"OMS_search_beta_ZC{z}_bgn{b}.pickle", "scripts/OMS_ldpc_search_best_beta.py:13-27", [-0.5])
+     for z in (12, 28, 40, 72, 176, 208) for b in (1, 2)] +
+    [("OMS_search_beta_ZC2_bgn1.pickle", "scripts/OMS_ldpc_search_best_beta.py:13 (commented list)", [-0.5])] +
+    [(f"mixed_MS_search_pair_ZC{z}_bgn{b}.pickle", "scripts/mixed_MS_ldpc_search_best_pair.py:13-27", [-1.0, -0.5])
+     for z, b in ((12, 1), (12, 2), (28, 1))] +
+    [("ldpc_decode_result_opt.pickle", "scripts/sim_ldpc_decoder.py:20-40 (L=32 run)", [-1.0, -0.5, 0.0, 0.5, 1.0]),
+     ("ldpc_decode_result_opt_2.pickle", "scripts/sim_ldpc_decoder.py:20-40", [-1.0, -0.5, 0.0, 0.5, 1.0]),
+     ("ldpc_decode_result_for_L.pickle", "scripts/sim_ldpc_decoder.py:57-81", [-1.0, -0.5, 0.0, 0.5])])
+
+
+def _parse_label(s):
+    """'NMS-alpha=0.7-L=32' / 'OMS-beta=0.5-L=16' / 'mixed-MS-[alpha,beta]=[0.8,0.3]-L=32' /
+    'BP L=32' / 'min-sum L=32' -> (algo, alpha, beta, L), the reverse of the reference's
+    label format (sim_ldpc_internal.py:15-41)."""
+    import re
+    m = re.fullmatch(r"NMS-alpha=([\d.]+)-L=(\d+)", s)
+    if m:
+        return "min-sum", float(m[1]), 0.0, int(m[2])
+    m = re.fullmatch(r"OMS-beta=([\d.]+)-L=(\d+)", s)
+    if m:
+        return "min-sum", 1.0, float(m[1]), int(m[2])
+    m = re.fullmatch(r"mixed-MS-\[alpha,beta\]=\[([\d.]+),([\d.]+)\]-L=(\d+)", s)
+    if m:
+        return "min-sum", float(m[1]), float(m[2]), int(m[3])
+    m = re.fullmatch(r"(BP|min-sum|BF) L=(\d+)", s)
+    return m[1], 1.0, 0.0, int(m[2])
+
+
+def gen_pins():
+    """tests/golden/bler_pins.json: every LDPC BLER value the reference published in out/."""
+    pins = []
+    for fname, src, snrs in PIN_FILES:
+        with open(os.path.join(REF, "out", fname), "rb") as fh:
+            cfg, labels, results = _NoGlobals(fh).load()
+        for lab, bl in zip(labels, results):
+            assert len(bl) == len(snrs), (fname, lab)
+            algo, alpha, beta, L = _parse_label(lab)
+            for snr, p in zip(snrs, bl):
+                pins.append({"file": "out/" + fname, "Zc": cfg["Zc"], "bgn": cfg["bgn"],
+                             "label": lab, "algo": algo, "alpha": alpha, "beta": beta, "L": L,
+                             "snr": snr, "bler": p, "config": src})
+    doc = {"_source": "BLER values the reference published in /root/reference/out/*.pickle "
+                      "(written by scripts/internal/sim_ldpc_internal.py:89-91), read by "
+                      "tests/golden/gen_golden.py gen_pins() with a no-globals unpickler; SNR "
+                      "lists from the scripts named in 'config'.  Every point is per-BPSK-symbol "
+                      "Es/N0 (nr_ldpc_decode.py:253-257), CRC24A, the reference's stopping rule "
+                      "(sim_ldpc_internal.py:66-77).",
+           "pins": pins}
+    with open(os.path.join(OUT, "bler_pins.json"), "w") as f:
+        json.dump(doc, f, indent=0)
+    print("bler pins", len(pins))
+
+
 if __name__ == "__main__":
     os.chdir(REF)
     sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
-    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "demod", "decode", "bfbp"]
+    which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "demod", "decode", "bfbp",
+                             "demod2", "config1", "pins"]
+    if "demod2" in which:
+        gen_demod2()
+    if "config1" in which:
+        gen_config1()
+    if "pins" in which:
+        gen_pins()
     if "encode" in which:
         gen_encode()
     if "crc" in which:

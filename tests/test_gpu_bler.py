@@ -1,51 +1,113 @@
 """Full-size statistical parity: the GPU BLER harness (python_5gtoolbox_amd.sim_ldpc, the batched
-run_ldpc_simulation of scripts/internal/sim_ldpc_internal.py:9-91) against the BLER values the
-reference published (tests/golden/bler_pins.json, from out/*.pickle via BASELINE.md §1).
+run_ldpc_simulation of scripts/internal/sim_ldpc_internal.py:9-91) against EVERY LDPC BLER value
+the reference published in out/*.pickle (tests/golden/bler_pins.json, 272 points: the NMS alpha
+and OMS beta searches over Zc 2..384 x BG1/BG2, the mixed (alpha, beta) searches, the algorithm
+comparison at Zc=12 L=16/32 and the iteration-count study at Zc=10).
 
-Decoding runs the float64 flooding kernel (the reference's schedule and arithmetic).  Each point
-uses the reference's own stopping rule, so both sides rest on the same trial counts n; the bar
-is a two-proportion test: |p - p_ref| <= 4 sqrt(q (1 - q) (2 / n)) + 1 / n, q the pooled rate."""
+Trials behind a published value: the pickles store only the BLER.  The harness's stopping rule
+stops at 1000/2000/4000/10000 codeblocks once 50/25/10 errors are seen (sim_ldpc_internal.py:
+66-77, np.array([200,400,800,2000])*5 and np.array([10,5,2])*5); a run with the unscaled lists
+(200/400/800/2000, 10/5/2) gives the same set of attainable values.  The test takes n_ref = the
+SMALLEST trial count consistent with the published value under either rule (the widest
+tolerance the data allow); our side always runs the x5 rule.
+
+Bars:
+  * flooding (the reference's schedule; float64, bit-exact per codeblock): two-sided,
+      |p - p_ref| <= 4 sqrt(q (1 - q) (1/n + 1/n_ref)) + 1/min(n, n_ref), q the pooled rate;
+  * layered (the perf kernel the headline benches; float32): one-sided at matched (alpha, beta,
+    L) — at least as good as the reference's flooding decoder,
+      p_layered <= p_ref + 4 sqrt(q (1 - q) (1/n + 1/n_ref)) + 1/min(n, n_ref),
+    at every attenuated operating point (alpha <= 0.8 or beta >= 0.3: all NMS/OMS/mixed values
+    the reference recommends).  Under-attenuated messages (alpha >= 0.9 with beta <= 0.1, i.e.
+    plain min-sum, NMS 0.9, OMS 0.1) make the layered schedule WORSE than flooding — a property
+    of row-serial min-sum (the over-estimated messages are reused within the same iteration),
+    reproduced by the CPU layered oracle; those points are checked for flooding
+    only, and test_layered_underattenuated_characterised records the direction.
+algo='BP' points run the float64 sum-product kernel (flooding only)."""
 import math
 
-import numpy as np
 import pytest
 
 from conftest import load_json
 
 pytestmark = pytest.mark.gpu
 
+PINS = load_json("bler_pins.json")["pins"]
+
 
 def _ref_trials(p):
-    """Trials the reference's stopping rule (sim_ldpc_internal.py:66-77) spends at BLER p."""
-    for n, lim in zip((1000, 2000, 4000), (50, 25, 10)):
-        if round(p * n) >= lim:
-            return n
-    return 10000
+    """Smallest trial count at which the reference's stopping rule (either scale, see above)
+    can have stopped with BLER exactly p."""
+    for sc in (1, 5):
+        for n, lim in zip((200 * sc, 400 * sc, 800 * sc, 2000 * sc), (10 * sc, 5 * sc, 2 * sc, 0)):
+            f = p * n
+            if abs(f - round(f)) < 1e-6 and round(f) >= lim:
+                return n
+    raise AssertionError(f"BLER {p} is not attainable under the reference's stopping rule")
 
 
-def _cases():
+def _attenuated(pin):
+    return pin["alpha"] <= 0.8 or pin["beta"] >= 0.3
+
+
+def _tol(n, f, p_ref):
+    n_ref = _ref_trials(p_ref)
+    q = (f + p_ref * n_ref) / (n + n_ref)
+    return 4 * math.sqrt(q * (1 - q) * (1 / n + 1 / n_ref)) + 1 / min(n, n_ref)
+
+
+def _cases(schedule):
     out = []
-    for pin in load_json("bler_pins.json")["pins"]:
-        key = "alpha" if pin["algo"] == "NMS" else "beta"
-        for v, b in zip(pin[key], pin["bler"]):
-            out.append((pin["Zc"], pin["bgn"], pin["algo"], pin["L"], pin["snr"], v, b))
+    for i, p in enumerate(PINS):
+        if schedule == "layered" and (p["algo"] != "min-sum" or not _attenuated(p)):
+            continue
+        out.append(pytest.param(i, p, id=f"{p['file'][4:-7]}-{p['label']}-snr{p['snr']}"))
     return out
 
 
-@pytest.mark.parametrize("Zc,bgn,algo,L,snr,v,p_ref", _cases())
-def test_bler_matches_reference_pins(Zc, bgn, algo, L, snr, v, p_ref):
+def _run(i, pin, schedule):
     import torch
     from python_5gtoolbox_amd.sim_ldpc import bler_point
     dev = torch.device("cuda", 0)
     gen = torch.Generator(device=dev)
-    gen.manual_seed(int(1000 * v) + Zc)
-    alpha, beta = (v, 0.0) if algo == "NMS" else (1.0, v)
-    n, f = bler_point(Zc, bgn, snr, "24A", "min-sum", alpha, beta, L, gen, dev)
-    p = f / n
-    n_ref = _ref_trials(p_ref)
-    q = (f + p_ref * n_ref) / (n + n_ref)
-    tol = 4 * math.sqrt(q * (1 - q) * (1 / n + 1 / n_ref)) + 1 / min(n, n_ref)
-    assert abs(p - p_ref) <= tol, (Zc, bgn, algo, v, n, f, p, p_ref, tol)
+    gen.manual_seed(7919 * i + (1 if schedule == "layered" else 0))
+    n, f = bler_point(pin["Zc"], pin["bgn"], pin["snr"], "24A", pin["algo"], pin["alpha"],
+                      pin["beta"], pin["L"], gen, dev, schedule)
+    return n, f
+
+
+@pytest.mark.parametrize("i,pin", _cases("flooding"))
+def test_bler_flooding_matches_reference(i, pin):
+    n, f = _run(i, pin, "flooding")
+    p, p_ref = f / n, pin["bler"]
+    assert abs(p - p_ref) <= _tol(n, f, p_ref), (pin, n, f, p)
+
+
+@pytest.mark.parametrize("i,pin", _cases("layered"))
+def test_bler_layered_at_least_reference(i, pin):
+    n, f = _run(i, pin, "layered")
+    p, p_ref = f / n, pin["bler"]
+    assert p - p_ref <= _tol(n, f, p_ref), (pin, n, f, p)
+
+
+def test_layered_underattenuated_characterised():
+    """At alpha = 0.9 (Zc=208 BG1, L=32, -0.5 dB: reference flooding BLER 0.145) the layered
+    schedule is worse than flooding on the same codeblocks, and at alpha = 0.75 better: the
+    direction DESIGN.md §2 states, measured on the GPU kernels with one codeblock set."""
+    import torch
+    from python_5gtoolbox_amd.nr_ldpc_decode import nr_decode_ldpc_batch
+    from python_5gtoolbox_amd.sim_ldpc import gen_codeblocks
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    blk, llr = gen_codeblocks(208, 1, -0.5, "24A", 2000, gen, dev)
+    err = {}
+    for a in (0.75, 0.9):
+        for sch, x in (("flooding", llr), ("layered", llr.float())):
+            ck, _, _ = nr_decode_ldpc_batch(x, 208, 1, 32, "min-sum", a, 0.0, sch)
+            err[a, sch] = int((ck[:, :blk.shape[1]] != blk).any(dim=1).sum().item())
+    assert err[0.9, "layered"] > err[0.9, "flooding"], err
+    assert err[0.75, "layered"] <= err[0.75, "flooding"], err
 
 
 def test_run_ldpc_simulation_shape(tmp_path):

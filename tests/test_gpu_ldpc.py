@@ -331,3 +331,33 @@ def test_decode_bp_batch_vs_oracle(torch, dec):
         assert np.array_equal(got[1], ref[1])
         both = ref[1]
         assert np.array_equal(got[0][both], ref[0][both]) and np.array_equal(got[2][both], ref[2][both])
+
+
+def test_config1_golden_dropins(torch, dec):
+    """BASELINE config 1 exactly (BG2 Zc=8, CRC24A, NMS alpha=.75, L=8), against the reference's
+    own outputs (tests/golden/config1_golden.npz): for_test_5g_ldpc_encoder under the same
+    np.random seed reproduces (blkandcrc, dn, LLR) bit for bit (host CRC + GPU
+    encoder), and nr_decode_ldpc (float64 flooding kernel) reproduces ck and status."""
+    from conftest import GOLD
+    d = np.load(f"{GOLD}/config1_golden.npz")
+    for i, seed in enumerate(d["seed"].tolist()):
+        np.random.seed(seed)
+        blk, dn, llr = dec.for_test_5g_ldpc_encoder(8, 2, float(d["snr"][i]), "24A")
+        assert np.array_equal(blk, d["blk"][i]) and np.array_equal(dn, d["dn"][i])
+        assert np.array_equal(llr.view(np.uint64), d["llr"][i].view(np.uint64))
+        blkandcrc, ck, status = dec.nr_decode_ldpc(llr, 8, 2, 8, "min-sum", 0.75, 0)
+        assert status == bool(d["status"][i]) and np.array_equal(ck, d["ck"][i]), i
+        assert np.shares_memory(blkandcrc, ck) and blkandcrc.size == 80
+
+
+def test_config1_layered_vs_oracle(torch, dec):
+    """Config 1 through the batched layered perf kernel: bit-exact vs the layered oracle, and
+    every codeblock the reference decoded is decoded to the same codeword."""
+    from conftest import GOLD
+    d = np.load(f"{GOLD}/config1_golden.npz")
+    llr = d["llr"].astype(np.float32)
+    ck, st, it = dec.nr_decode_ldpc_batch(llr, 8, 2, 8, "min-sum", 0.75, 0.0, "layered")
+    rck, rst, rit = O.decode_layered(llr, 8, 2, 8, 0.75, 0.0)
+    assert np.array_equal(ck, rck) and np.array_equal(st, rst) and np.array_equal(it, rit)
+    ref_ok = d["status"].astype(bool)
+    assert st[ref_ok].all() and np.array_equal(ck[ref_ok], d["ck"][ref_ok])

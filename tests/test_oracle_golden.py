@@ -166,3 +166,30 @@ def test_prbs_modulation_demodulation_golden():
         assert np.array_equal(O.modulate(bits, Qm).view(np.uint32), d[f"sym{k}"].view(np.uint32)), Qm
         llr = O.demodulate(d[f"y{k}"], d[f"nv{k}"], Qm)
         assert np.array_equal(llr.view(np.uint32), d[f"llr{k}"].view(np.uint32)), Qm
+
+
+def test_config1_golden_oracle():
+    """BASELINE config 1 (BG2 Zc=8, CRC24A, NMS alpha=.75, L=8): the reference's own
+    for_test_5g_ldpc_encoder + nr_decode_ldpc outputs (tests/golden/config1_golden.npz) are
+    reproduced by the oracle's CRC, encoder and float64 flooding decoder."""
+    d = np.load(f"{GOLD}/config1_golden.npz")
+    blk, dn, llr = d["blk"], d["dn"], d["llr"]
+    assert np.array_equal(O.encode(blk, 2), dn)
+    for i in range(blk.shape[0]):
+        assert np.array_equal(O.crc_encode(blk[i, :56], "24A"), blk[i])
+    ck, st, _ = O.decode_flooding(llr, 8, 2, 8, 0.75, 0.0, np.float64)
+    assert np.array_equal(st.astype(np.uint8), d["status"])
+    assert np.array_equal(ck, d["ck"])
+    assert 0 < d["status"].sum() < d["status"].size   # both outcomes covered
+
+
+def test_bler_pins_complete():
+    """Every LDPC BLER value the reference published is a pin (tests/golden/bler_pins.json)."""
+    pins = load_json("bler_pins.json")["pins"]
+    assert len(pins) == 272
+    files = {p["file"] for p in pins}
+    assert "out/ldpc_decode_result_opt.pickle" in files and "out/NMS_search_alpha_ZC384_bgn1.pickle" in files
+    assert {p["algo"] for p in pins} == {"min-sum", "BP"}
+    assert any(p["alpha"] < 1 and p["beta"] > 0 for p in pins)      # mixed min-sum
+    opt = [p["bler"] for p in pins if p["file"].endswith("_opt.pickle") and p["label"] == "NMS-alpha=0.7-L=32"]
+    assert opt == [0.395, 0.135, 0.015, 0.0005, 0.0]                # BASELINE.md §1
