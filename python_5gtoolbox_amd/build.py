@@ -39,8 +39,21 @@ def deps():
     return sources() + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "ldpc5g.h")]
 
 
+def _stamp():
+    """Everything besides the sources that decides the library's code: a library built with other
+    flags or for another arch (an A/B build into the default path) is never reused as the product."""
+    return " ".join([HIPCC, ARCH, *FLAGS, os.environ.get("LDPC5G_EXTRA_FLAGS", ""),
+                     os.environ.get("LDPC5G_SLP", ""), *sorted(NO_SLP)])
+
+
 def up_to_date():
     if not os.path.exists(LIB):
+        return False
+    try:
+        with open(LIB + ".stamp") as f:
+            if f.read() != _stamp():
+                return False
+    except OSError:
         return False
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(d) <= t for d in deps())
@@ -77,6 +90,9 @@ def build(force=False, verbose=True, csrc=None, out=None):
         print(" ".join(link), flush=True)
     subprocess.run(link, check=True)
     os.replace(lib_path + ".tmp", lib_path)
+    if not alt:
+        with open(LIB + ".stamp", "w") as f:
+            f.write(_stamp())
     return lib_path
 
 

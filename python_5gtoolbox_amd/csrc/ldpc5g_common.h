@@ -95,11 +95,9 @@ constexpr int kDecThreads = 384;   // = max Zc: one thread per check row z of a 
 constexpr int kCS = kDecThreads;   // LDS column stride (entries): G*Zc <= 384 always
 
 // layered float32 kernel: 768-thread workgroups (12 waves = 3 per SIMD at <= 168 VGPRs) holding
-// G = floor(768 / Zc) codeblocks, e.g. two BG1 Zc=384 codeblocks
-#ifndef LDPC5G_LAYERED_THREADS
-#define LDPC5G_LAYERED_THREADS 768   // A/B builds: -DLDPC5G_LAYERED_THREADS=384 (1 CB/workgroup, 2 workgroups/CU)
-#endif
-constexpr int kDecThreadsL = LDPC5G_LAYERED_THREADS;
+// G = floor(768 / Zc) codeblocks, e.g. two BG1 Zc=384 codeblocks (384-thread workgroups, two per
+// CU, measured 31 % slower: DESIGN.md §4.2)
+constexpr int kDecThreadsL = 768;
 inline int dec_threads(bool layered) { return layered ? kDecThreadsL : kDecThreads; }
 inline int dec_G(int Zc, bool layered = false) {
     const int T = dec_threads(layered);

@@ -117,33 +117,10 @@ constexpr bool xl_lds() { return sizeof(T) == 4 && !LAYERED; }
 // are held to fewer resident waves).  2 x (40 KB APP + 33 KB state + 3 KB flags) <= 160 KB.
 template <int BG>
 constexpr int lds_rows() { return BG == 1 ? 11 : 18; }
-// Layered rows with more edges than this recompute their rotated LDS addresses in pass 2
-// (LDPC5G_RECOMP_DEG overrides it at build time for A/B builds).
-#ifndef LDPC5G_RECOMP_DEG
-#define LDPC5G_RECOMP_DEG 12
-#endif
-constexpr int kRecompDeg = LDPC5G_RECOMP_DEG;
-// A/B switches (off by default; r01i, 4096 / 16384 CBs: 1.629 / 1.708 M CB/s without either,
-// 1.607 / 1.695 with BATCH_READS, 1.596 / 1.696 with OPAQUE_SW -- LDS latency is hidden by the
-// three waves per SIMD, the kernel is VALU-issue bound):
-//   LDPC5G_BATCH_READS: layered pass 1 issues all of a row's LDS reads before consuming any;
-//   LDPC5G_OPAQUE_SW:   prefetched shift words kept opaque (no scalar reload after the barrier);
-//   LDPC5G_SPLIT_MIN=d: rows of degree >= d run two two-min chains (r01n: 1.643 / 1.702 at d = 8,
-//                       1.636 / 1.679 at d = 5 vs 1.647 / 1.700 off -- no latency to remove).
-// Also measured and dropped (r01u): stop-rule flags double-buffered by iteration parity, so an
-// iteration without a convergence candidate ends with 2 barriers instead of 4 (1.600 / 1.701 vs
-// 1.638 / 1.711 M CB/s) -- barrier count is not what binds.  Scheduler flags (r01w):
-// -amdgpu-sched-strategy=max-ilp 1.566 / 1.629, -amdgpu-schedule-metric-bias=0 1.621 / 1.702 vs
-// 1.589 / 1.696 default (run-to-run noise ~2 %).
-#ifndef LDPC5G_BATCH_READS
-#define LDPC5G_BATCH_READS 0
-#endif
-#ifndef LDPC5G_OPAQUE_SW
-#define LDPC5G_OPAQUE_SW 0
-#endif
-#ifndef LDPC5G_SPLIT_MIN
-#define LDPC5G_SPLIT_MIN 0
-#endif
+// Layered rows with more edges than this recompute their rotated LDS addresses in pass 2.
+// (Variants measured and dropped are listed in DESIGN.md §4.2; tools/ab/make_variants.py rebuilds
+// them as separate libraries for side-by-side timing.)
+constexpr int kRecompDeg = 12;
 // LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
 template <bool LAYERED>
 constexpr int dec_cs() { return LAYERED ? kDecThreadsL : kDecThreads; }
@@ -154,7 +131,8 @@ constexpr size_t dec_lds_bytes_t() {
     constexpr size_t CS = dec_cs<LAYERED>();
     return (size_t)BGT<BG>::KC * CS * sizeof(T) * (LAYERED ? 1 : 2) +
            (xl_lds<T, LAYERED>() ? (size_t)(BGT<BG>::MB - 4) * CS * sizeof(T) : 0) +
-           (LAYERED ? (size_t)2 * lds_rows<BG>() * CS * sizeof(T) : 0) + (2 * kMaxG + 4) * sizeof(int);
+           (LAYERED ? (size_t)2 * lds_rows<BG>() * CS * sizeof(T) : 0) + (2 * kMaxG + 4) * sizeof(int) +
+           (LAYERED ? (size_t)2 * CS * sizeof(uint32_t) : 0);
 }
 
 // Layered state words: rows 0..3 one word each (negs | idx << 24); rows >= 4 (degree <= 12) two
@@ -205,6 +183,7 @@ __device__ __forceinline__ void dec_body(
     constexpr int ST_B = XL_B + (XL_LDS ? (MB - 4) * CS * TS : 0);   // layered: LDS row state
     constexpr int NLR = LAYERED ? lds_rows<BG>() : 0;
     constexpr int FLAG_B = ST_B + 2 * NLR * CS * TS;
+    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // layered: wrap table, 2*CS entries
     extern __shared__ __align__(16) unsigned char smem[];
 
     if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
@@ -344,6 +323,15 @@ __device__ __forceinline__ void dec_body(
     for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);
     if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
     if (t == 0) *anyf = 0;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    if constexpr (LAYERED) {   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
+        const int ZG = Zc * G;
+        if (t < ZG) {
+            *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + t * 4) = (uint32_t)(t * 4);
+            *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + (t + ZG) * 4) = (uint32_t)(t * 4);
+        }
+    }
+    const uint32_t tzbT = (uint32_t)(TBL_B + (valid ? t : 0) * 4);
     bool active = valid;
     lds_barrier();
 
@@ -452,57 +440,28 @@ __device__ __forceinline__ void dec_body(
             T q[d];
             int rb[d];
             T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-            // two independent two-min chains (even / odd edges) for long rows: half the
-            // dependent min/med3 latency (LDPC5G_SPLIT_MIN = smallest degree split, 0 = never)
-            constexpr bool SPLIT = LDPC5G_SPLIT_MIN > 0 && d >= LDPC5G_SPLIT_MIN;
-            T min1b = FT<T>::inf(), min2b = FT<T>::inf();
             uint32_t sx = 0;
-#if LDPC5G_BATCH_READS
-            // all of the row's rotated APP reads are issued before the first one is consumed, so
-            // the row waits for LDS latency once, not once per edge (lgkmcnt counts down)
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int j = P::COL[e0 + k];
-                if constexpr (j < KC) {
-                    rb[k] = rot(gshift(e0 + k));
-                    q[k] = at(j * CS * TS + rb[k]);
-                }
-            });
-            __builtin_amdgcn_sched_barrier(0);
-#endif
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
                 if constexpr (j < KC) {
                     const T sel = (idxo == (uint32_t)k) ? mBs : mAs;
                     const T rold = __uint_as_float(__builtin_amdgcn_bitop3_b32(u, __float_as_uint(sel), mv, 0x6c));
-#if LDPC5G_BATCH_READS
-                    q[k] = q[k] - rold;
-#else
-                    rb[k] = rot(gshift(e0 + k));
+                    // rotated entry (z + s) mod Zc: the wrap table maps the unwrapped offset
+                    rb[k] = (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)gshift(e0 + k) * GT);
                     q[k] = at(j * CS * TS + rb[k]) - rold;
-#endif
                 } else {
                     q[k] = xl;   // degree-1 column: q is the channel LLR itself
                 }
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
                 const T aq = fabs(q[k]);
-                if constexpr (SPLIT && (k & 1)) {
-                    min2b = FT<T>::med3(min1b, min2b, aq);
-                    min1b = fmin(min1b, aq);
-                } else {
-                    min2 = FT<T>::med3(min1, min2, aq);
-                    min1 = fmin(min1, aq);
-                }
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
                 if constexpr (k % 2 == 1)   // three-input XOR
                     sx = __builtin_amdgcn_bitop3_b32(sx, FT<T>::sbits(q[k - 1]), FT<T>::sbits(q[k]), 0x96);
                 else if constexpr (k == d - 1)
                     sx ^= FT<T>::sbits(q[k]);
             });
-            if constexpr (SPLIT) {   // merge the two chains: exact (selections only), ties kept
-                min2 = fmin(fmax(min1, min1b), fmin(min2, min2b));
-                min1 = fmin(min1, min1b);
-            }
             T x1 = min1, x2 = min2;
             if constexpr (OFS) {
                 x1 = min1 - beta, x2 = min2 - beta;
@@ -513,14 +472,11 @@ __device__ __forceinline__ void dec_body(
             uint32_t negs = 0, idxn = 0;
             // High-degree rows (BG1 rows 0-3, d = 19): keeping all d rotated addresses live from
             // pass 1 to pass 2 beside the d messages overflows the 168-VGPR budget (scratch spills
-            // reloaded inside the iteration loop); their addresses are recomputed from an opaque
-            // copy of the thread offsets instead (2 VALU per edge, no CSE with pass 1).
+            // reloaded inside the iteration loop); their addresses are looked up again from an
+            // opaque copy of the table base instead (1 VALU + 1 LDS read per edge, no CSE).
             constexpr bool RECOMP = d > kRecompDeg;
-            uint32_t tzb2 = (uint32_t)tzb, tzbw2 = tzbw;
-            if constexpr (RECOMP) {
-                asm volatile("" : "+v"(tzb2));
-                asm volatile("" : "+v"(tzbw2));
-            }
+            uint32_t tzbT2 = tzbT;
+            if constexpr (RECOMP) asm volatile("" : "+v"(tzbT2));
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
@@ -534,7 +490,7 @@ __device__ __forceinline__ void dec_body(
                 if constexpr (j < KC) {
                     if constexpr (RECOMP) {
                         const uint32_t S = (uint32_t)gshift(e0 + k) * GT;
-                        at(j * CS * TS + (int)min(tzb2 + S, tzbw2 + S)) = app;
+                        at(j * CS * TS + (int)*(lds_u32*)(uintptr_t)(tzbT2 + S)) = app;
                     } else {
                         at(j * CS * TS + rb[k]) = app;
                     }
@@ -556,11 +512,6 @@ __device__ __forceinline__ void dec_body(
             sfor<0, group_nw<BG>(g)>([&](auto wc) {
                 constexpr int w = decltype(wc)::value;
                 nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
-#if LDPC5G_OPAQUE_SW
-                // opaque: the compiler may not re-issue the constant load after the barrier
-                // (a scalar-cache round trip at the head of every row group)
-                asm volatile("" : "+s"(nsw[w]));
-#endif
             });
         };
         // layered: the ext-column LLRs of group g are loaded from global memory at the start of

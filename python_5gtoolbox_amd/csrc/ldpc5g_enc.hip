@@ -345,23 +345,10 @@ __device__ __forceinline__ uint32_t ext_word(const uint32_t* v, int base, int Zc
     return fetch_rot32(v, base, Zc, mod_zc(32 * q, Zc));
 }
 
-// 16-B store of encoder output; LDPC5G_ENC_NT=1 (A/B build) makes it non-temporal
-#ifndef LDPC5G_ENC_NT
-#define LDPC5G_ENC_NT 0
-#endif
-#ifndef LDPC5G_ENC_COAL
-#define LDPC5G_ENC_COAL 1   // lane-contiguous 16-B pieces for the info loads / stores (A/B switch)
-#endif
+// 16-B store of encoder output (non-temporal stores measured 2x slower)
 template <typename V>
 __device__ __forceinline__ void st16(int8_t* p, V v) {
-#if LDPC5G_ENC_NT
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    u4 x;
-    __builtin_memcpy(&x, &v, 16);
-    __builtin_nontemporal_store(x, (u4*)p);
-#else
     *(V*)p = v;
-#endif
 }
 
 // Bit-matrix transpose between "byte k of word q" and "bit 4q + k" orders, by four delta swaps
@@ -462,8 +449,8 @@ __device__ __forceinline__ void enc_sync() {
 }
 
 // Phases 2-6 of the fast encoder for one codeblock whose packed bits are in ib (LDS): parity
-// straight to dst.  LDSONLY: barriers order LDS only, so the systematic stores, parity stores and
-// (pipelined kernel) the next codeblock's loads stay in flight across them.
+// straight to dst.  LDSONLY: barriers order LDS only, so the systematic and parity stores stay in
+// flight across them.
 template <int BG, bool LDSONLY>
 __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_t* sm, int8_t* dst,
                                                 int Zc, int zi, int t, int NT) {
@@ -556,7 +543,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     // [32T, 32T + 32), so a wave's 64 tasks are 2 KB in a row.  Lane l then stores 16-byte piece l
     // and piece 64 + l of that range (words l/2 and 32 + l/2, fetched with two lane permutes):
     // each store instruction writes 1 KB contiguous instead of 16 B every 32 B.
-    const bool coal = LDPC5G_ENC_COAL && (Zc & 31) == 0 && (NT & 63) == 0;
+    const bool coal = (Zc & 31) == 0 && (NT & 63) == 0;
     const int lane = t & 63;
     int8_t* ext = dst + S + 4 * Zc;
     for (int task0 = t; task0 - lane < ntask; task0 += NT) {   // wave-uniform trip count
@@ -599,7 +586,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     // ---- 1. info bytes: pack parity bits; the systematic part is stored straight to dn.  Up to
     //      kEncChunks 32-B chunks per thread are loaded before any is used (one HBM round trip,
     //      not one per chunk); the phase-6 edge table is filled meanwhile.
-    if (LDPC5G_ENC_COAL && (NT & 63) == 0) {
+    if ((NT & 63) == 0) {
         // 16-byte pieces, lane-contiguous (piece p = half p & 1 of chunk p / 2): every load and
         // systematic store instruction moves 1 KB contiguous; the two halves of a chunk sit in
         // lanes l, l ^ 1 of the same wave and are joined with one lane exchange.
@@ -645,51 +632,6 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT);
 }
 
-// Pipelined persistent encoder: a workgroup encodes codeblocks b, b + grid, b + 2 grid, ...; the
-// next codeblock's information bytes are loaded into registers while the current one's parity
-// is computed and stored, so HBM reads, LDS work and HBM writes of consecutive codeblocks overlap
-// (the one-codeblock-per-workgroup kernel runs every CU's codeblocks through the same phase at
-// the same time).  256 threads, <= 2 chunks of 32 B per thread (K <= 8448).
-constexpr int kEncPipeNT = 256;
-template <int BG>
-__global__ __launch_bounds__(kEncPipeNT) void ldpc_enc_pipe_kernel(const int8_t* __restrict__ ck,
-                                                                   int8_t* __restrict__ dn, int B,
-                                                                   int Zc, int zi, int64_t ldk,
-                                                                   int64_t ldn) {
-    int b = blockIdx.x;
-    if (b >= B) return;
-    const int t = threadIdx.x;
-    const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
-    const int twoZ = 2 * Zc, KW = Ly.KW;
-    extern __shared__ __align__(16) uint32_t sm[];
-    int4 buf[2][2];
-    auto load = [&](int cb) {
-        const int8_t* src = ck + (int64_t)cb * ldk;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int wi = t + c * kEncPipeNT;
-            if (wi < KW) {
-                buf[c][0] = *(const int4*)(src + wi * 32);
-                buf[c][1] = *(const int4*)(src + wi * 32 + 16);
-            }
-        }
-    };
-    load(b);
-    enc_fill_ext_tab<BG>(sm, Ly, zi, t, kEncPipeNT);   // same for every codeblock (one zi)
-    for (; b < B; b += gridDim.x) {
-        int8_t* dst = dn + (int64_t)b * ldn;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const int wi = t + c * kEncPipeNT;
-            if (wi < KW) sm[wi] = enc_pack_chunk(buf[c], wi * 32, twoZ, dst);
-        }
-        if (t < 2) sm[KW + t] = 0;
-        if (b + (int)gridDim.x < B) load(b + gridDim.x);
-        lds_sync();
-        enc_fast_parity<BG, true>(Ly, sm, dst, Zc, zi, t, kEncPipeNT);
-        lds_sync();   // ib / X / lam / pv are rewritten by the next codeblock
-    }
-}
 }  // namespace
 
 int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,
@@ -697,54 +639,16 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
     const bool fast = (Zc % 16) == 0 && (ldk % 16) == 0 && (ldn % 16) == 0 &&
                       (((uintptr_t)ck) & 15) == 0 && (((uintptr_t)dn) & 15) == 0;
     if (fast) {
-        // LDPC5G_ENC_MODE (A/B switch): fast (default) | pipe | sync (fast with full barriers).
-        // Measured (r01c, 4096 x BG1 Zc=384): fast 40.2 us, sync 40.4 us, pipe 62.5 us (4 WG/CU),
-        // 61.1 us (8 WG/CU): the per-codeblock LDS/VALU critical path, not HBM, sets the time, so
-        // the most codeblocks in flight (one per workgroup) wins.
-        static const int mode = [] {
-            const char* e = getenv("LDPC5G_ENC_MODE");
-            if (e && !strcmp(e, "pipe")) return 0;
-            if (e && !strcmp(e, "sync")) return 2;
-            return 1;
-        }();
-        static const int nt = [] {
-            const char* e = getenv("LDPC5G_ENC_THREADS");
-            int v = e ? atoi(e) : 128;
-            return (v == 64 || v == 128 || v == 256) ? v : 128;
-        }();
-        if (mode == 0) {
-            static const int per_cu = [] {
-                const char* e = getenv("LDPC5G_ENC_WG_PER_CU");
-                int v = e ? atoi(e) : 4;
-                return v >= 1 && v <= 16 ? v : 4;
-            }();
-            int dev = 0, ncu = 256;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-            const int grid = std::min(B, ncu * per_cu);
-            if (bgn == 1)
-                hipLaunchKernelGGL(ldpc_enc_pipe_kernel<1>, dim3(grid), dim3(kEncPipeNT),
-                                   enc_fast_lds_bytes<1>(Zc), st, ck, dn, B, Zc, zi, ldk, ldn);
-            else
-                hipLaunchKernelGGL(ldpc_enc_pipe_kernel<2>, dim3(grid), dim3(kEncPipeNT),
-                                   enc_fast_lds_bytes<2>(Zc), st, ck, dn, B, Zc, zi, ldk, ldn);
-            return check_hip(hipGetLastError(), "ldpc_enc_pipe_kernel launch");
-        }
-        if (mode == 1) {
-            if (bgn == 1)
-                hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
-                                   st, ck, dn, B, Zc, zi, ldk, ldn);
-            else
-                hipLaunchKernelGGL((ldpc_enc_fast_kernel<2, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
-                                   st, ck, dn, B, Zc, zi, ldk, ldn);
-        } else {
-            if (bgn == 1)
-                hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, false>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
-                                   st, ck, dn, B, Zc, zi, ldk, ldn);
-            else
-                hipLaunchKernelGGL((ldpc_enc_fast_kernel<2, false>), dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
-                                   st, ck, dn, B, Zc, zi, ldk, ldn);
-        }
+        // one 128-thread workgroup per codeblock (measured r01c/r01m: a pipelined persistent
+        // variant 62 us, 256 threads +8 %, full barriers +0.5 % vs 25-40 us: the per-codeblock
+        // LDS/VALU critical path, not HBM, sets the time, so most codeblocks in flight wins)
+        constexpr int nt = 128;
+        if (bgn == 1)
+            hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
+                               st, ck, dn, B, Zc, zi, ldk, ldn);
+        else
+            hipLaunchKernelGGL((ldpc_enc_fast_kernel<2, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<2>(Zc),
+                               st, ck, dn, B, Zc, zi, ldk, ldn);
         return check_hip(hipGetLastError(), "ldpc_enc_fast_kernel launch");
     }
     if (bgn == 1)

@@ -63,6 +63,13 @@ def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
         it = t.empty((B,), dtype=t.int32, device=x.device)
     else:
         ck, st, it = out
+        # the C ABI trusts these buffers: wrong dtype / size / device would be out-of-bounds writes
+        assert ck.dtype == t.int8 and ck.dim() == 2 and ck.shape[0] == B and ck.shape[1] >= Nf \
+            and ck.stride(1) == 1, "out[0] must be int8 (B, >= Nf) with unit column stride"
+        assert st.dtype == t.uint8 and it.dtype == t.int32 and st.numel() >= B and it.numel() >= B \
+            and st.is_contiguous() and it.is_contiguous(), "out[1]/out[2] must be uint8/int32 (>= B,)"
+        assert ck.device == x.device and st.device == x.device and it.device == x.device, \
+            "outputs must live on the LLR tensor's device"
     flags = _lib.LLR_FULL if full else 0
     lib = _lib.lib()
     with t.cuda.device(x.device):

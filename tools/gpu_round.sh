@@ -51,15 +51,11 @@ if has trace; then
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
 fi
 if has probe; then
-  echo "[gpu_round] encoder A/B"
-  for m in pipe fast sync; do
-    LDPC5G_ENC_MODE=$m timeout -k 10 120 python -u tools/probe.py encode 4096 16384 > "$OUT/probe_enc_$m.log" 2>&1 || die probe $?
-    echo "$m: $(tr '\n' ' ' < "$OUT/probe_enc_$m.log")"
-  done
-  for w in 2 8; do
-    LDPC5G_ENC_WG_PER_CU=$w timeout -k 10 120 python -u tools/probe.py encode 4096 > "$OUT/probe_enc_pipe_w$w.log" 2>&1 || die probe $?
-    echo "pipe w$w: $(cat "$OUT/probe_enc_pipe_w$w.log")"
-  done
+  echo "[gpu_round] throughput probes"
+  timeout -k 10 120 python -u tools/probe.py encode 4096 16384 > "$OUT/probe_enc.log" 2>&1 || die probe $?
+  timeout -k 10 120 python -u tools/probe.py layered 4096 16384 > "$OUT/probe_layered.log" 2>&1 || die probe $?
+  timeout -k 10 120 python -u tools/probe.py flooding64 4096 > "$OUT/probe_flooding64.log" 2>&1 || die probe $?
+  grep -hv amdgpu.ids "$OUT"/probe_*.log
 fi
 if has ab; then
   echo "[gpu_round] decoder A/B builds (build/alt/*.so)"
