@@ -202,22 +202,30 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
 int ldpc5g_prbs(const uint32_t* cinit, int32_t T, int64_t nbits, uint32_t* words, int64_t ldw,
                 void* stream);
 
-/* Scrambling + modulation mapper (nr_pdsch_process.py:17-25, nrModulation.py:4-41), Qm = 2, 4,
- * 6, 8 (QPSK..256QAM): bits [T][ldb] int8 (nbits each) XOR prbs words (NULL: no scrambling) ->
- * complex64 symbols [T][ldsym] (float2), bit-exact with the reference's float32 arithmetic. */
+/* Modulation ids: the order Qm for QPSK..1024QAM, 1 for BPSK and LDPC5G_PI2_BPSK for pi/2-BPSK
+ * (nrModulation.py:14-42 / nr_Demodulation.py:30-43 accept all seven). */
+#define LDPC5G_PI2_BPSK (-1)
+
+/* Scrambling + modulation mapper (nr_pdsch_process.py:17-25, nrModulation.py:4-42), mod = 1, -1,
+ * 2, 4, 6, 8, 10: bits [T][ldb] int8 (nbits each, a multiple of Qm) XOR prbs words (NULL: no
+ * scrambling) -> complex64 symbols [T][ldsym] (float2), bit-exact with the reference's float32
+ * arithmetic (pi/2-BPSK: odd symbol index within each row rotated, :17-21). */
 int ldpc5g_scramble_modulate(const int8_t* bits, int64_t ldb, const uint32_t* prbs, int64_t ldw,
-                             int32_t T, int64_t nbits, int32_t Qm, void* sym, int64_t ldsym,
+                             int32_t T, int64_t nbits, int32_t mod, void* sym, int64_t ldsym,
                              void* stream);
 
-/* Soft demodulation (nr_Demodulation.py:12-46, demod_{qpsk,16qam,64qam,256qam}.py) + LLR
- * descrambling (nr_pdsch.py:268-274): symbols [T][ldsym] complex64 (LDPC5G_F32) or complex128
- * (LDPC5G_F64), noise variances [T][ldnv] float32 -> LLRs [T][ldllr] float32 (nsym*Qm each),
- * multiplied by 1 - 2c(n) when prbs is not NULL.  float64 arithmetic in the reference's order:
- * bit-exact with the reference on complex128 input. */
+/* Soft demodulation (nr_Demodulation.py:12-46, demod_{bpsk,pi2_bpsk,qpsk,16qam,64qam,256qam,
+ * 1024qam}.py) + LLR descrambling (nr_pdsch.py:268-274): symbols [T][ldsym] complex64
+ * (sym_dtype LDPC5G_F32) or complex128 (LDPC5G_F64), noise variances [T][ldnv] float32 -> LLRs
+ * [T][ldllr] (nsym*Qm each), multiplied by 1 - 2c(n) when prbs is not NULL.  The arithmetic
+ * follows the reference's operation order in the symbols' precision: float64 for complex128;
+ * float32 for complex64 with every constant (k*A, c*A, threshold*A) rounded to float32 first, as
+ * numpy >= 2 evaluates demod_*.py then.  llr_dtype LDPC5G_F32 always works; LDPC5G_F64 is accepted
+ * for BPSK on complex128 input, whose reference LLRs are float64 (demod_bpsk.py:9). */
 int ldpc5g_demod_descramble(const void* sym, int32_t sym_dtype, int64_t ldsym,
                             const float* noise_var, int64_t ldnv, const uint32_t* prbs,
-                            int64_t ldw, int32_t T, int64_t nsym, int32_t Qm, float* llr,
-                            int64_t ldllr, void* stream);
+                            int64_t ldw, int32_t T, int64_t nsym, int32_t mod, void* llr,
+                            int32_t llr_dtype, int64_t ldllr, void* stream);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* ldpc5g_last_error(void);

@@ -22,6 +22,7 @@ Contents (reference file:line each restates):
                                               py5gphy/ldpc/nr_ldpc_raterecover.py:6-65
   cbsegment ...................... py5gphy/ldpc/nr_ldpc_cbsegment.py:7-33
 """
+import json
 import math
 import os
 
@@ -690,33 +691,43 @@ def prbs(c_init, N):
     return (x1[1600:1600 + N] ^ x2[1600:1600 + N]).astype(np.int8)
 
 
-_QAM_SCALE = {2: 2, 4: 10, 6: 42, 8: 170}
+# modulation id (ABI convention): the order Qm for QPSK..1024QAM, 1 BPSK, -1 pi/2-BPSK
+_QAM_SCALE = {-1: 2, 1: 2, 2: 2, 4: 10, 6: 42, 8: 170, 10: 682}
 
 
-def modulate(bits, Qm):
-    """nrModulate (py5gphy/common/nrModulation.py:4-41) for QPSK..256QAM: float32 levels, then
-    numpy's complex64 division by the real scalar sqrt(scale), which multiplies by the float32
-    reciprocal 1 / float32(sqrt(scale)) (Smith's algorithm with a zero imaginary divisor)."""
+def modulate(bits, mod):
+    """nrModulate (py5gphy/common/nrModulation.py:4-42), all seven: float32 levels, then numpy's
+    complex64 division by the real scalar sqrt(scale), which multiplies by the float32 reciprocal
+    1 / float32(sqrt(scale)) (Smith's algorithm with a zero imaginary divisor)."""
+    Qm = abs(mod)
     b = np.asarray(bits).astype(np.float32).reshape(-1, Qm)
     u = 1 - 2 * b                                   # float32
-    if Qm == 2:
+    if Qm == 1:
+        re, im = u[:, 0].copy(), u[:, 0]
+        if mod == -1:                               # pi/2-BPSK: odd symbols (2b - 1) + j(1 - 2b)
+            re[1::2] = 2 * b[1::2, 0] - 1
+    elif Qm == 2:
         re, im = u[:, 0], u[:, 1]
     elif Qm == 4:
         re, im = u[:, 0] * (2 - u[:, 2]), u[:, 1] * (2 - u[:, 3])
     elif Qm == 6:
         re = u[:, 0] * (4 - u[:, 2] * (2 - u[:, 4]))
         im = u[:, 1] * (4 - u[:, 3] * (2 - u[:, 5]))
-    else:
+    elif Qm == 8:
         re = u[:, 0] * (8 - u[:, 2] * (4 - u[:, 4] * (2 - u[:, 6])))
         im = u[:, 1] * (8 - u[:, 3] * (4 - u[:, 5] * (2 - u[:, 7])))
-    scl = np.float32(1) / np.float32(math.sqrt(_QAM_SCALE[Qm]))
+    else:
+        re = u[:, 0] * (16 - u[:, 2] * (8 - u[:, 4] * (4 - u[:, 6] * (2 - u[:, 8]))))
+        im = u[:, 1] * (16 - u[:, 3] * (8 - u[:, 5] * (4 - u[:, 7] * (2 - u[:, 9]))))
+    scl = np.float32(1) / np.float32(math.sqrt(_QAM_SCALE[mod]))
     return (re * scl + 1j * (im * scl)).astype(np.complex64)
 
 
-# Piecewise-linear soft-demodulation segments of demod_{qpsk,16qam,64qam,256qam}.py, per PAM
-# bit pair p (bits 2p / 2p+1 from the real / imaginary part): (upper threshold in units of A,
+# Piecewise-linear soft-demodulation segments of demod_{qpsk,16qam,64qam,256qam,1024qam}.py, per
+# PAM bit pair p (bits 2p / 2p+1 from the real / imaginary part): (upper threshold in units of A,
 # k, s, c) meaning  r < thr*A  ->  LLR = (k*A) * (s*r + (s*c)*A) / noise_var  (= s (k A)(r + c A)
 # / noise_var up to the sign of zero, which follows the reference's written form; c = 0: (k*A)*r).
+# 1024QAM: oracle/demod1024_segments.json (tools/gen_demod_tables.py, from demod_1024qam.py).
 _INF = float("inf")
 DEMOD_SEGMENTS = {
     2: [[(_INF, 4, 1, 0)]],
@@ -739,24 +750,41 @@ DEMOD_SEGMENTS = {
         [(-12, 4, 1, 14), (-8, 4, -1, 10), (-4, 4, 1, 6), (0, 4, -1, 2), (4, 4, 1, -2),
          (8, 4, -1, -6), (12, 4, 1, -10), (_INF, 4, -1, -14)]],
 }
+with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "demod1024_segments.json")) as _f:
+    DEMOD_SEGMENTS[10] = [[(_INF if t is None else t, k, s, c) for t, k, s, c in segs]
+                          for segs in json.load(_f)["segments"]]
 
 
-def demodulate(sym, noise_var, Qm):
-    """nrDemodulate (demodulation/nr_Demodulation.py:12-46 -> demod_*.py) for QPSK..256QAM:
-    float64 arithmetic in the reference's operation order, stored as float32."""
-    y = np.asarray(sym, np.complex128).reshape(-1)
-    nv = np.asarray(noise_var).real.reshape(-1).astype(np.float32).astype(np.float64)
-    A = 1 / math.sqrt(_QAM_SCALE[Qm])
+def demodulate(sym, noise_var, mod):
+    """nrDemodulate (demodulation/nr_Demodulation.py:12-46 -> demod_*.py), all seven, in the
+    reference's precision: the expressions are evaluated on numpy arrays of the symbols' real
+    type with the reference's Python-float constants, so numpy (>= 2, NEP 50) applies the same
+    rules as to the reference's scalars: float64 for complex128 input, float32 (constants and
+    thresholds rounded to float32) for complex64.  Returns float32 LLRs, except BPSK on
+    complex128 input: float64 (demod_bpsk.py:9 stores nothing)."""
+    y = np.asarray(sym).reshape(-1)
+    if y.dtype != np.complex64:
+        y = y.astype(np.complex128)
+    nv = np.asarray(noise_var).real.reshape(-1).astype(np.float32)
+    Qm = abs(mod)
+    A = 1 / math.sqrt(_QAM_SCALE[mod])
+    re, im = y.real, y.imag
+    if mod == 1:
+        return 4 * (re + im) * A / nv
     out = np.zeros(y.size * Qm, np.float32)
+    if mod == -1:
+        out[0::2] = 4 * (re[0::2] + im[0::2]) * A / nv[0::2]
+        out[1::2] = 4 * (-re[1::2] + im[1::2]) * A / nv[1::2]
+        return out
     for p, segs in enumerate(DEMOD_SEGMENTS[Qm]):
-        thr = np.array([t * A if t != _INF else _INF for t, _, _, _ in segs[:-1]])
-        for part, r in ((0, y.real), (1, y.imag)):
-            reg = np.searchsorted(thr, r, side="right")
-            v = np.zeros(r.size)
-            for i, (_, k, s, c) in enumerate(segs):
-                m = reg == i
+        for part, r in ((0, re), (1, im)):
+            v = np.zeros(r.size, r.dtype)
+            done = np.zeros(r.size, bool)
+            for t, k, s, c in segs:      # the if / elif chain: first segment with r < t*A
+                m = ~done if t == _INF else (~done) & (r < t * A)
                 x = r[m] if c == 0 else s * r[m] + (s * c) * A
-                v[m] = ((k * A) * x) / nv[m]
+                v[m] = (k * A) * x / nv[m]
+                done |= m
             out[2 * p + part::Qm] = v
     return out
 

@@ -66,8 +66,8 @@ SIGNATURES = {
                                             _c.c_int64, _c.c_void_p]),
     "ldpc5g_demod_descramble": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p,
                                            _c.c_int64, _c.c_void_p, _c.c_int64, _c.c_int32,
-                                           _c.c_int64, _c.c_int32, _c.c_void_p, _c.c_int64,
-                                           _c.c_void_p]),
+                                           _c.c_int64, _c.c_int32, _c.c_void_p, _c.c_int32,
+                                           _c.c_int64, _c.c_void_p]),
     "ldpc5g_last_error": (_c.c_char_p, []),
     "ldpc5g_version": (_c.c_char_p, []),
 }

@@ -49,26 +49,58 @@ def test_demodulation_dropin_vs_reference(torch, gold):
         assert np.array_equal(hard, np.where(ref > 0, 0, 1)), mod
 
 
-@pytest.mark.parametrize("Qm", [2, 4, 6, 8])
-def test_batched_scramble_modulate_and_demod_descramble_vs_oracle(torch, Qm):
+MOD_IDS = {"bpsk": 1, "pi/2-bpsk": -1, "qpsk": 2, "16qam": 4, "64qam": 6, "256qam": 8, "1024qam": 10}
+
+
+def _raw(a):
+    a = np.asarray(a)
+    return a.view(np.uint64 if a.dtype.itemsize == 8 else np.uint32)
+
+
+@pytest.fixture(scope="module")
+def gold2():
+    return np.load(f"{GOLD}/demod2_golden.npz")
+
+
+def test_all_modulations_dropins_vs_reference(torch, gold2):
+    """nrModulate / nrDemodulate drop-ins for all seven modulations of the reference (BPSK,
+    pi/2-BPSK and 1024QAM included) against its own outputs, raw bits: complex64 symbols; LLRs
+    for complex128 input (float64 arithmetic; BPSK returned as float64 like demod_bpsk.py) and
+    complex64 input (float32 arithmetic, numpy >= 2)."""
+    from python_5gtoolbox_amd import nrModulation, nr_Demodulation
+    mods = gold2["mods"].tolist()
+    for k, Qm, n in gold2["meta"].tolist():
+        bits = np.unpackbits(gold2[f"bits{k}"])[:n * Qm]
+        sym = nrModulation.nrModulate(bits, mods[k].upper())
+        assert sym.dtype == np.complex64 and np.array_equal(_raw(sym), _raw(gold2[f"sym{k}"])), mods[k]
+        for key, y in ((f"llr{k}", gold2[f"y{k}"]), (f"llr_c64_{k}", gold2[f"y{k}"].astype(np.complex64))):
+            hard, llr = nr_Demodulation.nrDemodulate(y, mods[k], gold2[f"nv{k}"])
+            ref = gold2[key]
+            assert llr.dtype == ref.dtype and np.array_equal(_raw(llr), _raw(ref)), (mods[k], key)
+            assert np.array_equal(hard, np.where(ref > 0, 0, 1)), (mods[k], key)
+
+
+@pytest.mark.parametrize("mod", [1, -1, 2, 4, 6, 8, 10])
+def test_batched_scramble_modulate_and_demod_descramble_vs_oracle(torch, mod):
     from python_5gtoolbox_amd import phy
-    rng = np.random.default_rng(Qm)
+    Qm = abs(mod)
+    rng = np.random.default_rng(Qm + 20 * (mod < 0))
     T, nsym = 3, 5003
     cinit = [12345 * 2 ** 15 + 17, 1, 2 ** 31 - 1]
     ct = torch.tensor(cinit, dtype=torch.int64, device="cuda")
     bits = rng.integers(0, 2, (T, nsym * Qm)).astype(np.int8)
-    sym = phy.scramble_modulate(torch.from_numpy(bits).cuda(), Qm, ct).cpu().numpy()
+    sym = phy.scramble_modulate(torch.from_numpy(bits).cuda(), mod, ct).cpu().numpy()
     for t in range(T):
-        ref = O.modulate(bits[t] ^ O.prbs(cinit[t], bits.shape[1]), Qm)
+        ref = O.modulate(bits[t] ^ O.prbs(cinit[t], bits.shape[1]), mod)
         assert np.array_equal(sym[t].view(np.uint32), ref.view(np.uint32)), t
     y = sym.astype(np.complex128) + 0.05 * (rng.normal(size=sym.shape) + 1j * rng.normal(size=sym.shape))
     nv = rng.uniform(0.01, 0.5, sym.shape).astype(np.float32)
     for dt in (torch.complex128, torch.complex64):
         yy = y if dt == torch.complex128 else y.astype(np.complex64)
-        llr = phy.demod_descramble(torch.from_numpy(yy).cuda(), torch.from_numpy(nv).cuda(), Qm,
+        llr = phy.demod_descramble(torch.from_numpy(yy).cuda(), torch.from_numpy(nv).cuda(), mod,
                                    ct).cpu().numpy()
         for t in range(T):
-            ref = O.descramble(O.demodulate(yy[t], nv[t], Qm), cinit[t])
+            ref = O.descramble(O.demodulate(yy[t], nv[t], mod).astype(np.float32), cinit[t])
             assert np.array_equal(llr[t].view(np.uint32), ref.view(np.uint32)), (dt, t)
 
 

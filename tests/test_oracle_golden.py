@@ -168,6 +168,30 @@ def test_prbs_modulation_demodulation_golden():
         assert np.array_equal(llr.view(np.uint32), d[f"llr{k}"].view(np.uint32)), Qm
 
 
+MOD_IDS = {"bpsk": 1, "pi/2-bpsk": -1, "qpsk": 2, "16qam": 4, "64qam": 6, "256qam": 8, "1024qam": 10}
+
+
+def _raw(a):
+    a = np.asarray(a)
+    return a.view(np.uint64 if a.dtype.itemsize == 8 else np.uint32)
+
+
+def test_all_modulations_golden_oracle():
+    """modulate / demodulate restatements == the reference's nrModulate / nrDemodulate for all
+    seven modulations (tests/golden/demod2_golden.npz), with complex128 AND complex64 symbols
+    (float64 vs float32 arithmetic), raw bits compared, output dtypes included."""
+    d = np.load(os.path.join(GOLD, "demod2_golden.npz"))
+    mods = d["mods"].tolist()
+    for k, Qm, n in d["meta"].tolist():
+        mod = MOD_IDS[mods[k]]
+        bits = np.unpackbits(d[f"bits{k}"])[:n * Qm]
+        assert np.array_equal(_raw(O.modulate(bits, mod)), _raw(d[f"sym{k}"])), mods[k]
+        for key, y in ((f"llr{k}", d[f"y{k}"]), (f"llr_c64_{k}", d[f"y{k}"].astype(np.complex64))):
+            llr = O.demodulate(y, d[f"nv{k}"], mod)
+            ref = d[key]
+            assert llr.dtype == ref.dtype and np.array_equal(_raw(llr), _raw(ref)), (mods[k], key)
+
+
 def test_config1_golden_oracle():
     """BASELINE config 1 (BG2 Zc=8, CRC24A, NMS alpha=.75, L=8): the reference's own
     for_test_5g_ldpc_encoder + nr_decode_ldpc outputs (tests/golden/config1_golden.npz) are
