@@ -26,6 +26,7 @@ K_INFO, N_TX, N_FULL = 22 * ZC, 66 * ZC, 68 * ZC
 EDGES = 316 * ZC
 DEC_BYTES_PER_CB = 4 * N_TX + N_FULL + 1 + 4       # f32 LLR in, int8 ck out, status, iters
 ENC_BYTES_PER_CB = K_INFO + N_TX                     # int8 bits in, int8 dn out
+DEC64_BYTES_PER_CB = 8 * N_TX + N_FULL + 1 + 4       # f64 LLR in, int8 ck out, status, iters
 HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip table (spec)
 # rocprofv3 PMC summary of this code version (tools/gpu_round.sh pmc step -> tools/pmc_summary.py),
 # committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
@@ -48,6 +49,7 @@ def pmc_traffic(kernel, corrected16=False):
 
 
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12        # 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T/s
+ALG_OPS_PER_EDGE = 13                                # lane-ops per edge-update
 
 
 def pmc_valu_insts(kernel):
@@ -194,6 +196,33 @@ def cpu_baseline(seconds, schedule, alpha, L, procs):
                         "(BASELINE.md §2); the reference cannot travel to the GPU box"}}
 
 
+def bench_config1(rank, n=300):
+    """BASELINE config 1 shape on the GPU: ONE BG2 Zc=8 codeblock per call through the
+    reference-style drop-ins (numpy in / numpy out, as scripts/internal/sim_ldpc_internal.py:51-58
+    calls them): us per encode_ldpc and per nr_decode_ldpc (float64 flooding, NMS alpha=.75,
+    L=8), host round trip included.  The reference itself: 1.2-2.2 ms per encode, 30-57 ms per
+    decode on one core."""
+    import numpy as np
+    from python_5gtoolbox_amd import nr_ldpc_decode as D, nr_ldpc_encode as E
+    rng = np.random.default_rng(7 + rank)
+    ck = rng.integers(0, 2, 80).astype(np.int8)
+    llr = 2 * ((1 - 2 * E.encode_ldpc(ck.copy(), 2)) + 0.8 * rng.normal(size=400)) / 0.64
+    for _ in range(20):
+        E.encode_ldpc(ck.copy(), 2)
+        D.nr_decode_ldpc(llr, 8, 2, 8, "min-sum", 0.75, 0)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        E.encode_ldpc(ck.copy(), 2)
+    t1 = time.perf_counter()
+    for _ in range(n):
+        D.nr_decode_ldpc(llr, 8, 2, 8, "min-sum", 0.75, 0)
+    t2 = time.perf_counter()
+    return {"workload": "BASELINE config 1: single BG2 Zc=8 codeblock per call, drop-in API",
+            "encode_us_per_call": round((t1 - t0) / n * 1e6, 1),
+            "decode_us_per_call": round((t2 - t1) / n * 1e6, 1), "calls": n,
+            "reference_cpu_ms_per_call": {"encode": "1.2-2.2", "decode": "30-57"}}
+
+
 def bench_config4(torch, dist, world, dev, rank, steps):
     """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
     (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
@@ -333,6 +362,7 @@ def main():
     launch_s = ev / args.steps
     achieved = B * DEC_BYTES_PER_CB / launch_s / 1e9
     edge_rate = B * EDGES * iters / launch_s
+    alg_lane_ops = edge_rate * ALG_OPS_PER_EDGE
     res = {
         "metric": "LDPC codeblocks/s + info-Gbit/s, BG1 Zc=384 NMS L=8, 1/2/4/8 MI355X",
         "value": round(value, 1),
@@ -353,16 +383,22 @@ def main():
                    "snr_db": args.snr, "mean_iterations": round(iters, 3),
                    "converged": conv, "parallelism": f"cb-shard x{world}"},
         "info_gbit_s": round(value * K_INFO / 1e9, 3),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "roofline": {"bound": "valu", "achieved": round(alg_lane_ops / 1e12, 3),
+                     "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
+                     "frac": round(alg_lane_ops / 1e12 / VALU_PEAK_TLANE, 4),
                      "traffic": pmc_traffic(DEC_KERNEL[args.schedule]) if B == 4096 else None,
+                     "kernel": DEC_KERNEL[args.schedule], "launch_ms": round(launch_s * 1e3, 4),
+                     "algorithmic": f"{ALG_OPS_PER_EDGE} lane-ops per edge-update (SURVEY.md "
+                                    f"§8(d)) x 121,344 edges x mean iterations per codeblock",
+                     "hbm_achieved_GBps": round(achieved, 2), "hbm_peak_GBps": HBM_PEAK_GBS,
+                     "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "algorithmic_bytes_per_cb": DEC_BYTES_PER_CB,
                      "traffic_source": "profiles/pmc_latest.json: FETCH_SIZE + WRITE_SIZE bytes "
                                        "per 4096-CB launch (raw; FETCH includes Infinity-Cache "
                                        "hits of the per-iteration ext-column LLR re-reads)",
-                     "kernel": DEC_KERNEL[args.schedule],
-                     "algorithmic_bytes_per_cb": DEC_BYTES_PER_CB,
-                     "launch_ms": round(launch_s * 1e3, 4),
-                     "note": "decode is VALU/LDS-bound (~99 lane-op/B); see valu"},
+                     "note": "decode is VALU-bound (~99 lane-op/B, SURVEY.md finding 8): frac is "
+                             "the algorithmic lane-op rate against the full-rate VALU peak; the "
+                             "measured instruction rate is in `valu`"},
         "valu": valu_block(edge_rate, launch_s, DEC_KERNEL[args.schedule], B),
     }
 
@@ -396,10 +432,23 @@ def main():
                                    out=out)
         n2b = max(3, args.steps // 4)
         w2b, _ = timed(torch, dist, world, step2b, n2b, 1)
+        f64_launch = w2b / n2b
         ex[f"flooding_f64_snr{args.snr:g}dB"] = {
             "codeblocks_per_s": round(B * world * n2b / w2b, 1),
             "mean_iterations": round(out[2].float().mean().item(), 3),
-            "note": "float64 flooding = the reference's algorithm and arithmetic, bit-exact"}
+            "ms_per_call": round(f64_launch * 1e3, 4),
+            "note": "float64 flooding = the reference's algorithm and arithmetic, bit-exact "
+                    "(what nr_decode_ldpc / DLSCHDecode / ULSCH_decoding run)",
+            "roofline": {"bound": "valu",
+                         "achieved": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12, 3),
+                         "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
+                         "frac": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12
+                                       / VALU_PEAK_TLANE, 4),
+                         "kernel": "void ldpc_dec_kernel<1, double, false>",
+                         "hbm_achieved_GBps": round(B * DEC64_BYTES_PER_CB / f64_launch / 1e9, 2),
+                         "algorithmic_bytes_per_cb": DEC64_BYTES_PER_CB,
+                         "note": "same 13 lane-ops per edge-update in float64 against the "
+                                 "full-rate lane peak (wall time incl. launch)"}}
         del llr64
         # BASELINE config 2: encode-only
         dnb = torch.empty((B, N_TX), dtype=torch.int8, device=dev)
@@ -420,6 +469,20 @@ def main():
                                              if B == 4096 else None,
                                              "kernel": ENC_KERNEL,
                                              "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB}}
+        ex["config1_per_codeblock"] = bench_config1(rank)
+        tm = {}
+        from python_5gtoolbox_amd.shard import decode_codeblocks_sharded
+        if world == 1 or dist.get_backend() == "nccl":   # gloo cannot gather device tensors
+            for _ in range(2):   # second run timed (first allocates)
+                decode_codeblocks_sharded(llr, ZC, BG, args.L, args.alpha, 0.0, args.schedule,
+                                          n_total=B * world, timing=tm)
+        if tm:
+            ex["multi_gpu_gather"] = {
+                "what": "decode this rank's shard, pack info bits + status + iterations into "
+                        "1061-B records on the GPU, ONE dist.gather (RCCL) to rank 0, unpack there",
+                "gather_ms": round(tm["gather_s"] * 1e3, 3),
+                "decode_ms": round(tm["decode_s"] * 1e3, 3),
+                "gather_bytes": tm["gather_bytes"], "ranks": world}
         ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2))
         ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
         res["extras"] = ex

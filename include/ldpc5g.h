@@ -100,11 +100,29 @@ typedef struct {
 
 /* Decode a batch of codeblocks with heterogeneous (bgn, Zc) in at most two launches (one per
  * base graph).  `desc` is a HOST array of B descriptors; status[b] / iters[b] follow desc order.
- * The library keeps a small internal device work list (grown on demand, one per device). */
+ * The work list is built on the host, copied with a stream-ordered allocation
+ * (hipMallocAsync / hipMemcpyAsync / hipFreeAsync on `stream`): asynchronous and reentrant, no
+ * host synchronisation.  Repeated decodes of one batch shape should build the plan once instead
+ * (ldpc5g_mixed_plan + ldpc5g_decode_ms_mixed_plan). */
 int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* llr_base,
                            int32_t llr_dtype, int8_t* ck_base, uint8_t* status, int32_t* iters,
                            int32_t L, double alpha, double beta, int32_t schedule,
                            int32_t flags, void* stream);
+
+/* Build the work list (plan) of a mixed batch into the caller's HOST buffer `plan` (pinned memory
+ * recommended, `plan_bytes` long).  Returns the plan size in bytes (>= 0; the buffer is untouched
+ * when it is too small, so a first call with plan_bytes = 0 sizes it) or a negative error.  The
+ * plan depends only on (desc, B, schedule). */
+int64_t ldpc5g_mixed_plan(const ldpc5g_cb_desc_t* desc, int32_t B, int32_t schedule, void* plan,
+                          int64_t plan_bytes);
+
+/* Decode with a plan the caller copied to the device (`plan_dev`, the bytes ldpc5g_mixed_plan
+ * wrote, on this stream's device): <= 2 launches, nothing else — no allocation, no copy, no
+ * synchronisation.  schedule must be the one the plan was built for. */
+int ldpc5g_decode_ms_mixed_plan(const void* plan_dev, const void* plan_host, const void* llr_base,
+                                int32_t llr_dtype, int8_t* ck_base, uint8_t* status,
+                                int32_t* iters, int32_t L, double alpha, double beta,
+                                int32_t schedule, int32_t flags, void* stream);
 
 /* ============================================================ DL-SCH / UL-SCH transport chain
  * TS 38.212 §7.2 (DL-SCH) / §6.2 (UL-SCH) around the codec, batched over T transport blocks that
@@ -226,6 +244,22 @@ int ldpc5g_demod_descramble(const void* sym, int32_t sym_dtype, int64_t ldsym,
                             const float* noise_var, int64_t ldnv, const uint32_t* prbs,
                             int64_t ldw, int32_t T, int64_t nsym, int32_t mod, void* llr,
                             int32_t llr_dtype, int64_t ldllr, void* stream);
+
+/* ================================================ gather records (multi-GPU)
+ * Record r (a row of rec, stride ldr bytes) = the nbits int8 bits of row r of `bits` (values 0/1)
+ * packed in np.packbits order (bit i -> byte i/8, bit 7 - i%8, tail zero-padded), then
+ * status[r] (one byte, if status != NULL), then iters[r] (int32 little-endian, if iters != NULL).
+ * One record per codeblock (bits = its K info bits) or per transport block (its tbblk + CRC
+ * flag): a rank's results become one contiguous block for a single gather.  unpack reverses it;
+ * any of bits / status / iters may be NULL there to skip that field.  No reference counterpart
+ * (the reference runs in one process); the unpacked bits are the reference's blkandcrc / tbblk
+ * (nr_ldpc_decode.py:47-49, nr_dlsch_decode.py:103-109). */
+int ldpc5g_pack_records(const int8_t* bits, int64_t ldb, int32_t R, int64_t nbits,
+                        const uint8_t* status, const int32_t* iters, uint8_t* rec, int64_t ldr,
+                        void* stream);
+int ldpc5g_unpack_records(const uint8_t* rec, int64_t ldr, int32_t R, int64_t nbits, int8_t* bits,
+                          int64_t ldb, uint8_t* status, int32_t* iters, int64_t fstride,
+                          void* stream);   /* status / iters of record r at [r * fstride] */
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* ldpc5g_last_error(void);

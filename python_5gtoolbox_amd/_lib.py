@@ -5,6 +5,7 @@ the hot path.  There is no CPU fallback: if the library or a GPU is missing, cal
 """
 import ctypes
 import os
+import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LDPC5G_LIB") or os.path.join(HERE, "libldpc5g.so")
@@ -30,6 +31,11 @@ SIGNATURES = {
                                           _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
                                           _c.c_double, _c.c_double, _c.c_int32, _c.c_int32,
                                           _c.c_void_p]),
+    "ldpc5g_mixed_plan": (_c.c_int64, [_c.c_void_p, _c.c_int32, _c.c_int32, _c.c_void_p, _c.c_int64]),
+    "ldpc5g_decode_ms_mixed_plan": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                               _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                               _c.c_double, _c.c_double, _c.c_int32, _c.c_int32,
+                                               _c.c_void_p]),
     "ldpc5g_decode_bf": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                     _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
                                     _c.c_int64, _c.c_int64, _c.c_void_p]),
@@ -68,6 +74,12 @@ SIGNATURES = {
                                            _c.c_int64, _c.c_void_p, _c.c_int64, _c.c_int32,
                                            _c.c_int64, _c.c_int32, _c.c_void_p, _c.c_int32,
                                            _c.c_int64, _c.c_void_p]),
+    "ldpc5g_pack_records": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int32, _c.c_int64,
+                                       _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
+                                       _c.c_void_p]),
+    "ldpc5g_unpack_records": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int32, _c.c_int64,
+                                         _c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_void_p,
+                                         _c.c_int64, _c.c_void_p]),
     "ldpc5g_last_error": (_c.c_char_p, []),
     "ldpc5g_version": (_c.c_char_p, []),
 }
@@ -156,3 +168,19 @@ def stream_ptr(device=None):
 
 def ptr(tensor):
     return ctypes.c_void_p(tensor.data_ptr())
+
+
+_tls = threading.local()
+
+
+def staging(key, make):
+    """Per-thread cache of pinned-host / device buffers for the per-codeblock drop-ins (the
+    reference's callers decode one codeblock per call, sim_ldpc_internal.py:51-58): a call then
+    costs one pinned H2D copy, the launch and one D2H copy, with no allocation."""
+    d = getattr(_tls, "bufs", None)
+    if d is None:
+        d = _tls.bufs = {}
+    b = d.get(key)
+    if b is None:
+        b = d[key] = make()
+    return b

@@ -305,7 +305,7 @@ int launch_bp_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
     auto kern = ldpc_bp_kernel<BG>;
     const int G = dec_G(Zc);
     const size_t lds = (size_t)2 * P::KC * kCS * sizeof(double) + kCS * sizeof(int);
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (int rc = set_lds_once<ldpc_bp_kernel<BG>>(lds)) return rc;
     const int threads = ((G * Zc + 63) / 64) * 64;
     hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(threads), lds, st, llr, ck, status, iters,
                        msg, B, Zc, zi, G, ldl, ldc, L, pc);

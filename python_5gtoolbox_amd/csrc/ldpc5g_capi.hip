@@ -6,7 +6,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -40,13 +39,84 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 namespace {
-// per-device scratch for the mixed path's work lists
-struct MixedScratch {
-    void* dev = nullptr;
-    size_t cap = 0;
+// Mixed-batch plan layout (host bytes, copied verbatim to the device):
+//   MixedPlanHdr | DecWork[nw1] (BG1) | DecWork[nw2] (BG2) | CbRef[nref]
+struct MixedPlanHdr {
+    int32_t magic, schedule, nw1, nw2, nref, pad;
 };
-std::mutex g_mix_mu;
-MixedScratch g_mix[64];
+constexpr int32_t kPlanMagic = 0x4c504d58;   // "XMPL"
+
+int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out, int64_t cap) {
+    // group codeblocks by (bgn, Zc), pack G = floor(threads/Zc) per workgroup
+    std::vector<std::vector<int>> bucket[2];
+    bucket[0].resize(LDPC5G_NUM_ZC);
+    bucket[1].resize(LDPC5G_NUM_ZC);
+    for (int b = 0; b < B; ++b) {
+        const ldpc5g_cb_desc_t& d = desc[b];
+        if (d.bgn != 1 && d.bgn != 2) return fail(LDPC5G_EBGN, "desc[%d]: bgn must be 1 or 2 (got %d)", b, d.bgn);
+        const int zi = zc_index(d.Zc);
+        if (zi < 0) return fail(LDPC5G_EZC, "desc[%d]: Zc=%d is not a lifting size", b, d.Zc);
+        if (d.llr_off < 0 || d.ck_off < 0) return fail(LDPC5G_ESIZE, "desc[%d]: negative offset", b);
+        bucket[d.bgn - 1][zi].push_back(b);
+    }
+    std::vector<DecWork> work[2];
+    std::vector<CbRef> refs;
+    for (int g = 0; g < 2; ++g)
+        for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
+            const std::vector<int>& v = bucket[g][zi];
+            const int Zc = kLdpcZcList[zi], G = dec_G(Zc, schedule == LDPC5G_LAYERED);
+            for (size_t s = 0; s < v.size(); s += G) {
+                DecWork w;
+                w.zi = zi, w.Zc = Zc, w.G = (int)std::min<size_t>(G, v.size() - s), w.first = (int)refs.size();
+                for (int c = 0; c < w.G; ++c) {
+                    CbRef r;
+                    r.llr_off = desc[v[s + c]].llr_off, r.ck_off = desc[v[s + c]].ck_off, r.out = v[s + c], r.pad = 0;
+                    refs.push_back(r);
+                }
+                work[g].push_back(w);
+            }
+        }
+    const int64_t need = (int64_t)sizeof(MixedPlanHdr) + (int64_t)(work[0].size() + work[1].size()) * (int64_t)sizeof(DecWork) +
+                         (int64_t)refs.size() * (int64_t)sizeof(CbRef);
+    if (!out || cap < need) return need;
+    unsigned char* p = (unsigned char*)out;
+    MixedPlanHdr h{kPlanMagic, schedule, (int32_t)work[0].size(), (int32_t)work[1].size(), (int32_t)refs.size(), 0};
+    memcpy(p, &h, sizeof h);
+    p += sizeof h;
+    for (int g = 0; g < 2; ++g) {
+        memcpy(p, work[g].data(), work[g].size() * sizeof(DecWork));
+        p += work[g].size() * sizeof(DecWork);
+    }
+    memcpy(p, refs.data(), refs.size() * sizeof(CbRef));
+    return need;
+}
+
+// launches of a plan (host copy `h` for the counts, device copy `dev` for the kernels)
+int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr_base, int llr_dtype,
+                int8_t* ck_base, uint8_t* status, int32_t* iters, int L, double alpha, double beta,
+                int pc, hipStream_t st) {
+    const DecWork* w1 = (const DecWork*)(dev + sizeof(MixedPlanHdr));
+    const DecWork* w2 = w1 + h.nw1;
+    const CbRef* r = (const CbRef*)(w2 + h.nw2);
+    const bool lay = h.schedule == LDPC5G_LAYERED;
+    for (int g = 0; g < 2; ++g) {
+        const int nwg = g == 0 ? h.nw1 : h.nw2;
+        if (!nwg) continue;
+        if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
+                                      g == 0 ? w1 : w2, r, L, alpha, beta, pc, st))
+            return rc;
+    }
+    return LDPC5G_OK;
+}
+
+int check_mixed_args(int32_t B, int32_t L, int32_t llr_dtype, int32_t schedule, double beta) {
+    if (B < 0 || L < 0) return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d", B, L);
+    if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
+    if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
+    if (schedule == LDPC5G_LAYERED && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "layered schedule requires float32 LLRs");
+    if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
+    return LDPC5G_OK;
+}
 }  // namespace
 
 }  // namespace ldpc5g_impl
@@ -154,86 +224,51 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
                            void* stream) {
     g_err.clear();
     const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
-    if (B < 0 || L < 0) return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d", B, L);
-    if (llr_dtype != LDPC5G_F64 && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "bad llr dtype %d", llr_dtype);
-    if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
-    if (schedule == LDPC5G_LAYERED && llr_dtype != LDPC5G_F32) return fail(LDPC5G_ESIZE, "layered schedule requires float32 LLRs");
-    if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
+    if (int rc = check_mixed_args(B, L, llr_dtype, schedule, beta)) return rc;
     if (B == 0) return LDPC5G_OK;
     if (!desc || !llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
-    // group codeblocks by (bgn, Zc), pack G = floor(threads/Zc) per workgroup
-    std::vector<std::vector<int>> bucket[2];
-    bucket[0].resize(LDPC5G_NUM_ZC);
-    bucket[1].resize(LDPC5G_NUM_ZC);
-    for (int b = 0; b < B; ++b) {
-        const ldpc5g_cb_desc_t& d = desc[b];
-        if (d.bgn != 1 && d.bgn != 2) return fail(LDPC5G_EBGN, "desc[%d]: bgn must be 1 or 2 (got %d)", b, d.bgn);
-        int zi = zc_index(d.Zc);
-        if (zi < 0) return fail(LDPC5G_EZC, "desc[%d]: Zc=%d is not a lifting size", b, d.Zc);
-        if (d.llr_off < 0 || d.ck_off < 0) return fail(LDPC5G_ESIZE, "desc[%d]: negative offset", b);
-        bucket[d.bgn - 1][zi].push_back(b);
-    }
-    std::vector<DecWork> work[2];
-    std::vector<CbRef> refs;
-    for (int g = 0; g < 2; ++g)
-        for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
-            const std::vector<int>& v = bucket[g][zi];
-            const int Zc = kLdpcZcList[zi], G = dec_G(Zc, schedule == LDPC5G_LAYERED);
-            for (size_t s = 0; s < v.size(); s += G) {
-                DecWork w;
-                w.zi = zi, w.Zc = Zc, w.G = (int)std::min<size_t>(G, v.size() - s), w.first = (int)refs.size();
-                for (int c = 0; c < w.G; ++c) {
-                    CbRef r;
-                    r.llr_off = desc[v[s + c]].llr_off, r.ck_off = desc[v[s + c]].ck_off, r.out = v[s + c], r.pad = 0;
-                    refs.push_back(r);
-                }
-                work[g].push_back(w);
-            }
-        }
-    const size_t wbytes = (work[0].size() + work[1].size()) * sizeof(DecWork);
-    const size_t rbytes = refs.size() * sizeof(CbRef);
-    const size_t need = wbytes + rbytes;
-    int dev = 0;
-    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
-    hipStream_t st = (hipStream_t)stream;
+    const int64_t need = build_plan(desc, B, schedule, nullptr, 0);
+    if (need < 0) return (int)need;
     std::vector<unsigned char> host(need);
-    memcpy(host.data(), work[0].data(), work[0].size() * sizeof(DecWork));
-    memcpy(host.data() + work[0].size() * sizeof(DecWork), work[1].data(), work[1].size() * sizeof(DecWork));
-    memcpy(host.data() + wbytes, refs.data(), rbytes);
-    unsigned char* dbuf;
-    {
-        std::lock_guard<std::mutex> lk(g_mix_mu);
-        MixedScratch& s = g_mix[dev & 63];
-        if (s.cap < need) {
-            if (s.dev) {
-                (void)hipDeviceSynchronize();
-                (void)hipFree(s.dev);
-            }
-            s.dev = nullptr;
-            s.cap = 0;
-            if (int rc = check_hip(hipMalloc(&s.dev, need * 2), "hipMalloc(work list)")) return rc;
-            s.cap = need * 2;
-        }
-        dbuf = (unsigned char*)s.dev;
-        // the work list is consumed by this call's kernels; a later call on another stream
-        // would overwrite it, so the copy + launches are serialised on this stream and the
-        // host waits for the copy before returning the buffer to the pool
-        if (int rc = check_hip(hipMemcpyAsync(dbuf, host.data(), need, hipMemcpyHostToDevice, st), "hipMemcpyAsync(work list)")) return rc;
-        const DecWork* w1 = (const DecWork*)dbuf;
-        const DecWork* w2 = w1 + work[0].size();
-        const CbRef* r = (const CbRef*)(dbuf + wbytes);
-        const bool lay = schedule == LDPC5G_LAYERED;
-        for (int g = 0; g < 2; ++g) {
-            const int nwg = (int)work[g].size();
-            if (!nwg) continue;
-            const DecWork* w = g == 0 ? w1 : w2;
-            int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg, w, r,
-                                      L, alpha, beta, pc, st);
-            if (rc) return rc;
-        }
-        if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize(mixed)")) return rc;
-    }
-    return LDPC5G_OK;
+    build_plan(desc, B, schedule, host.data(), need);
+    MixedPlanHdr h;
+    memcpy(&h, host.data(), sizeof h);
+    hipStream_t st = (hipStream_t)stream;
+    // stream-ordered scratch: allocated, filled, used and freed in stream order; the pageable
+    // source is staged by hipMemcpyAsync before it returns, so `host` may go out of scope
+    void* dev = nullptr;
+    if (int rc = check_hip(hipMallocAsync(&dev, need, st), "hipMallocAsync(work list)")) return rc;
+    int rc = check_hip(hipMemcpyAsync(dev, host.data(), need, hipMemcpyHostToDevice, st), "hipMemcpyAsync(work list)");
+    if (!rc) rc = launch_plan(h, (const unsigned char*)dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc, st);
+    const int rc2 = check_hip(hipFreeAsync(dev, st), "hipFreeAsync(work list)");
+    return rc ? rc : rc2;
+}
+
+int64_t ldpc5g_mixed_plan(const ldpc5g_cb_desc_t* desc, int32_t B, int32_t schedule, void* plan,
+                          int64_t plan_bytes) {
+    g_err.clear();
+    if (B < 0) return fail(LDPC5G_ESIZE, "B=%d", B);
+    if (schedule != LDPC5G_FLOODING && schedule != LDPC5G_LAYERED) return fail(LDPC5G_ESIZE, "bad schedule %d", schedule);
+    if (B > 0 && !desc) return fail(LDPC5G_ESIZE, "null desc");
+    return build_plan(desc, B, schedule, plan, plan_bytes);
+}
+
+int ldpc5g_decode_ms_mixed_plan(const void* plan_dev, const void* plan_host, const void* llr_base,
+                                int32_t llr_dtype, int8_t* ck_base, uint8_t* status,
+                                int32_t* iters, int32_t L, double alpha, double beta,
+                                int32_t schedule, int32_t flags, void* stream) {
+    g_err.clear();
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    if (!plan_host || !plan_dev) return fail(LDPC5G_ESIZE, "null plan");
+    MixedPlanHdr h;
+    memcpy(&h, plan_host, sizeof h);
+    if (h.magic != kPlanMagic) return fail(LDPC5G_ESIZE, "not a mixed plan (ldpc5g_mixed_plan)");
+    if (h.schedule != schedule) return fail(LDPC5G_ESIZE, "plan built for schedule %d, called with %d", h.schedule, schedule);
+    if (int rc = check_mixed_args(h.nref, L, llr_dtype, schedule, beta)) return rc;
+    if (h.nref == 0) return LDPC5G_OK;
+    if (!llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
+    return launch_plan(h, (const unsigned char*)plan_dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc,
+                       (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -4,6 +4,7 @@
 
 #include <stdint.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "ldpc5g_tables.h"
@@ -109,6 +110,21 @@ int fail(int code, const char* fmt, ...);
 void clear_error();
 int zc_index(int Zc);
 int check_hip(hipError_t e, const char* what);
+
+// Raise kernel KERN's dynamic-LDS limit to `lds` bytes once per device: hipFuncSetAttribute is a
+// host-side round trip that the per-codeblock drop-in calls would otherwise pay on every launch.
+template <auto KERN>
+int set_lds_once(size_t lds) {
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return 0;
+    const hipError_t e = hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return check_hip(e, "hipFuncSetAttribute");
+    done.fetch_or(bit, std::memory_order_release);
+    return 0;
+}
 
 // ---- launchers (one per translation unit)
 int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, int64_t ldk,

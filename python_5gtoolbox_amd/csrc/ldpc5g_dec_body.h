@@ -7,6 +7,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "ldpc5g_common.h"
 
 namespace ldpc5g_impl {
@@ -698,11 +700,15 @@ template <int BG, typename T, bool LAYERED>
 int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                  int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
     auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
-    const int G = dec_G(Zc, LAYERED);
+    // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
+    // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
+    const int G = std::min(dec_G(Zc, LAYERED), B);
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     const int threads = ((G * Zc + 63) / 64) * 64;
     const int grid = (B + G - 1) / G;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false>()>(lds))
+        return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, llr, ck, status, iters, B, Zc, zi,
                        G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
                        (const CbRef*)nullptr);
@@ -715,7 +721,9 @@ int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters
                        int pc, hipStream_t st) {
     auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false>()>(lds))
+        return rc;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(dec_cs<LAYERED>()), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
     return check_hip(hipGetLastError(), "ldpc_dec_kernel(mixed) launch");
@@ -725,7 +733,7 @@ template <int BG, typename T, bool LAYERED>
 int blocks_per_cu_t() {
     auto kern = dec_kernel<BG, T, LAYERED>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (set_lds_once<dec_kernel<BG, T, LAYERED>()>(lds)) return -1;
     int n = -1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, dec_cs<LAYERED>(), lds) != hipSuccess) return -1;
     return n;

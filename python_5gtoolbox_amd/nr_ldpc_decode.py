@@ -96,6 +96,31 @@ def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
     return ck, st, it
 
 
+def _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, full):
+    """One codeblock through the float64 flooding kernel (the reference-exact path) with pinned
+    staging: LLRs -> pinned -> device, decode into one device record (ck | status | iters), one
+    D2H of that record.  Returns (ck int8 (Nf,), status bool)."""
+    t = _lib.require_gpu()
+    K, N, Nf = code_dims(bgn, Zc)
+    n_in = Nf if full else N
+    dev = t.cuda.current_device()
+
+    def make():
+        return (t.empty((1, n_in), dtype=t.float64, pin_memory=True),
+                t.empty((1, n_in), dtype=t.float64, device=dev),
+                t.empty((Nf + 8,), dtype=t.uint8, device=dev),
+                t.empty((Nf + 8,), dtype=t.uint8, pin_memory=True))
+    hin, din, drec, hrec = _lib.staging(("dec1", dev, n_in, Nf), make)
+    hin.numpy()[0] = np.asarray(LLRin, np.float64).reshape(-1)
+    din.copy_(hin, non_blocking=True)
+    out = (drec[:Nf].view(t.int8).view(1, Nf), drec[Nf:Nf + 1], drec[Nf + 4:Nf + 8].view(t.int32))
+    nr_decode_ldpc_batch(din, Zc, bgn, L, algo, alpha, beta, "flooding", full=full, out=out)
+    hrec.copy_(drec, non_blocking=True)
+    t.cuda.current_stream().synchronize()
+    h = hrec.numpy()
+    return h[:Nf].view(np.int8).copy(), bool(h[Nf])
+
+
 def nr_decode_ldpc(LLRin, Zc, bgn, L, algo="min-sum", alpha=1, beta=0):
     """LDPC decode following TS 38.212 5.3.2 — drop-in for nr_ldpc_decode.nr_decode_ldpc.
 
@@ -109,12 +134,10 @@ def nr_decode_ldpc(LLRin, Zc, bgn, L, algo="min-sum", alpha=1, beta=0):
     iLS = find_iLS(Zc)
     assert iLS < 8
     _check_algo(algo)
-    ck, st, _ = nr_decode_ldpc_batch(np.asarray(LLRin, np.float64).reshape(1, N), Zc, bgn, L,
-                                     algo, alpha, beta, "flooding")
-    ck = ck[0]
+    ck, st = _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, False)
     if algo == "BF":
         ck = ck.astype(np.float64)   # the reference's BF decisions are a float copy of LLRin
-    return ck[0:K], ck, bool(st[0])
+    return ck[0:K], ck, st
 
 
 def decode_ldpc(LLRin, H, L, algo="min-sum", alpha=1, beta=0):
@@ -128,10 +151,9 @@ def decode_ldpc(LLRin, H, L, algo="min-sum", alpha=1, beta=0):
     if m is None:
         raise NotImplementedError("decode_ldpc: H is not a TS 38.212 base-graph expansion")
     bgn, Zc = m
-    ck, st, _ = nr_decode_ldpc_batch(np.asarray(LLRin, np.float64).reshape(1, Ncol), Zc, bgn, L,
-                                     algo, alpha, beta, "flooding", full=True)
-    ck = ck[0].astype(np.float64) if algo == "BF" else ck[0]
-    return ck, bool(st[0])
+    ck, st = _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, True)
+    ck = ck.astype(np.float64) if algo == "BF" else ck
+    return ck, st
 
 
 def for_test_5g_ldpc_encoder(Zc, bgn, snr_db, crcpoly="24A"):

@@ -74,13 +74,32 @@ class MixedBatch:
         self.status = t.empty(max(B, 1), dtype=t.uint8, device=dev)
         self.iters = t.empty(max(B, 1), dtype=t.int32, device=dev)
         self.B = B
+        self._plans = {}
+
+    def _plan(self, schedule):
+        """Work list for `schedule`, built on the host once (pinned) and copied to the device
+        once; later decodes only launch (ldpc5g_decode_ms_mixed_plan)."""
+        p = self._plans.get(schedule)
+        if p is None:
+            t = _lib.torch()
+            lib = _lib.lib()
+            sc = _lib.LAYERED if schedule == "layered" else _lib.FLOODING
+            n = lib.ldpc5g_mixed_plan(self.desc, self.B, sc, None, 0)
+            _lib.check(int(min(n, 0)))
+            host = t.empty((max(n, 1),), dtype=t.uint8, pin_memory=True)
+            _lib.check(int(min(lib.ldpc5g_mixed_plan(self.desc, self.B, sc, _lib.ptr(host), n), 0)))
+            dev = host.to(self.llr.device, non_blocking=True)
+            p = self._plans[schedule] = (host, dev)
+        return p
 
     def decode(self, L, alpha=1.0, beta=0.0, schedule="layered"):
-        """One ldpc5g_decode_ms_mixed call (<= 2 kernel launches; returns after they finish)."""
+        """<= 2 kernel launches on the current stream, asynchronous (no host synchronisation);
+        returns the device buffers (ck flat, status (B,), iters (B,))."""
         t = _lib.torch()
+        host, dev = self._plan(schedule)
         with t.cuda.device(self.llr.device):
-            _lib.check(_lib.lib().ldpc5g_decode_ms_mixed(
-                self.desc, self.B, _lib.ptr(self.llr), _lib.F32, _lib.ptr(self.ck),
+            _lib.check(_lib.lib().ldpc5g_decode_ms_mixed_plan(
+                _lib.ptr(dev), _lib.ptr(host), _lib.ptr(self.llr), _lib.F32, _lib.ptr(self.ck),
                 _lib.ptr(self.status), _lib.ptr(self.iters), int(L), float(alpha), float(beta),
                 _lib.LAYERED if schedule == "layered" else _lib.FLOODING, 0,
                 _lib.stream_ptr(self.llr.device)))

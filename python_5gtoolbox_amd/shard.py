@@ -1,16 +1,25 @@
-"""Multi-GPU codeblock sharding: one process per GPU, codeblocks split into contiguous ranges,
-no collective on the data path, one gather of the decoded bits to rank 0 at the end.
+"""Multi-GPU sharding: one process per GPU, work split with no collective on the data path, one
+gather of packed results to rank 0 at the end (BASELINE.json north_star: "RCCL only for the final
+gather").
 
 The reference decodes codeblocks one at a time in a Python loop (py5gphy/nr_pdsch/
-nr_dlsch_decode.py:62-103); codeblocks are independent until the transport-block CRC (:106),
-so the batch axis shards with no exchange.  Transport blocks (config 5) shard whole, round
-robin, so each TB's CRC stays rank-local.
+nr_dlsch_decode.py:62-103); codeblocks are independent until the transport-block CRC (:106), so
+the batch axis shards with no exchange:
+  * codeblocks (configs 2-4): contiguous row ranges (shard_bounds);
+  * transport blocks (config 5): whole TBs round robin (shard_round_robin), so every TB's CRC
+    stays rank-local.
+Each rank packs its results on its GPU into gather records (ldpc5g_pack_records: np.packbits
+order, plus status / iteration fields — 1061 B per BG1 Zc=384 codeblock instead of 8448 B of
+info bytes), and ONE dist.gather (RCCL over xGMI; gloo in the CPU tests) brings every rank's
+record block to rank `dst`, which unpacks them on its GPU in shard order.
 
-torch.distributed is plumbing here: backend "nccl" (= RCCL over xGMI) on the GPU box, "gloo"
-in the CPU tests.  The per-rank decode is the HIP batch decoder unless a test passes its own
-`decode_fn`.
+torch.distributed and torch tensors are plumbing (device buffers, the collective); the packing
+and unpacking are HIP kernels.  Tests on CPU (gloo, no GPU) inject `decode_fn` / `pack_fn` /
+`unpack_fn` (numpy) — the product path requires the GPU.
 """
-import numpy as np
+import time
+
+from . import _lib
 
 
 def shard_bounds(n, rank, world):
@@ -27,31 +36,87 @@ def shard_round_robin(n, rank, world):
     return list(range(rank, n, world))
 
 
-def _gather_rows(torch, dist, local, n_total, world, group):
-    """all_gather of variable-length row blocks (padded to the largest shard) -> (n_total, ...)
-    on every rank; rank order = shard order."""
-    counts = [shard_bounds(n_total, r, world) for r in range(world)]
-    m = max(hi - lo for lo, hi in counts)
-    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
-    return torch.cat([b[:hi - lo] for b, (lo, hi) in zip(bufs, counts)], dim=0)
+def record_bytes(nbits, status=True, iters=True):
+    """Bytes of one gather record (include/ldpc5g.h ldpc5g_pack_records)."""
+    return (nbits + 7) // 8 + (1 if status else 0) + (4 if iters else 0)
+
+
+def pack_records(bits, nbits, status=None, iters=None, out=None):
+    """bits (R, >= nbits) int8 device tensor (+ status (R,) uint8, iters (R,) int32) -> records
+    (R, record_bytes) uint8 on the same device (`out` may have more rows: only R are written)."""
+    t = _lib.require_gpu()
+    R = bits.shape[0]
+    rb = record_bytes(nbits, status is not None, iters is not None)
+    rec = out if out is not None else t.empty((R, rb), dtype=t.uint8, device=bits.device)
+    assert rec.dtype == t.uint8 and rec.shape[0] >= R and rec.shape[1] >= rb and rec.stride(1) == 1
+    assert bits.dtype == t.int8 and bits.stride(1) == 1 and bits.shape[1] >= nbits
+    with t.cuda.device(bits.device):
+        for r0 in range(0, max(R, 1), 65535):   # grid.y limit
+            n = min(65535, R - r0)
+            if n <= 0:
+                break
+            _lib.check(_lib.lib().ldpc5g_pack_records(
+                _lib.ptr(bits[r0:]), bits.stride(0), n, int(nbits),
+                _lib.ptr(status[r0:]) if status is not None else None,
+                _lib.ptr(iters[r0:]) if iters is not None else None,
+                _lib.ptr(rec[r0:]), rec.stride(0), _lib.stream_ptr(bits.device)))
+    return rec
+
+
+def unpack_records(rec, R, nbits, bits=None, status=None, iters=None):
+    """Inverse of pack_records into the given device tensors (any may be None; bits rows and the
+    1-D status / iters may be strided views, e.g. every world-th TB)."""
+    t = _lib.require_gpu()
+    fs = (status if status is not None else iters).stride(0) if (status is not None or iters is not None) else 1
+    assert iters is None or status is None or iters.stride(0) == status.stride(0)
+    assert bits is None or (bits.dtype == t.int8 and bits.stride(1) == 1)
+    with t.cuda.device(rec.device):
+        for r0 in range(0, max(R, 1), 65535):
+            n = min(65535, R - r0)
+            if n <= 0:
+                break
+            _lib.check(_lib.lib().ldpc5g_unpack_records(
+                _lib.ptr(rec[r0:]), rec.stride(0), n, int(nbits),
+                _lib.ptr(bits[r0:]) if bits is not None else None,
+                bits.stride(0) if bits is not None else 0,
+                _lib.ptr(status[r0:]) if status is not None else None,
+                _lib.ptr(iters[r0:]) if iters is not None else None, fs,
+                _lib.stream_ptr(rec.device)))
+
+
+def gather_record_blocks(torch, dist, rec, counts, rank, world, dst=0, group=None):
+    """ONE dist.gather of every rank's record block (padded to the largest shard) to `dst`.
+    rec: (m, rb) uint8 with m = max(counts) rows, this rank's counts[rank] first.  Returns on dst
+    the (world, m, rb) buffer (rank r's records in [r, :counts[r]]), None elsewhere."""
+    assert rec.shape[0] >= max(counts)
+    buf = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device) \
+        if rank == dst else None
+    dist.gather(rec, gather_list=list(buf.unbind(0)) if buf is not None else None, dst=dst,
+                group=group)
+    return buf
+
+
+def _world(group):
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
 
 
 def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="layered",
-                              n_total=None, decode_fn=None, group=None, dst=0):
+                              n_total=None, decode_fn=None, pack_fn=None, unpack_fn=None,
+                              group=None, dst=0, timing=None):
     """Decode this rank's shard of a codeblock batch and gather the results to rank `dst`.
 
-    llr: this rank's (n_local, N) LLR rows (torch tensor on this rank's device), or the full
-         (n_total, N) batch, in which case the rank slices its own range.
+    llr: this rank's (n_local, N) LLR rows (device tensor), or the full (n_total, N) batch, in
+         which case the rank slices its own range.
     Returns on rank dst: (info bits (n_total, K) int8, status (n_total,) uint8,
-    iters (n_total,) int32); None on other ranks."""
+    iters (n_total,) int32) on dst's device; None on other ranks.  `timing` (dict) receives
+    decode_s / gather_s measured on this rank (synchronised wall clock)."""
     import torch
     import torch.distributed as dist
     from .ldpc_info import code_dims
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world, rank = _world(group)
     K, N, Nf = code_dims(bgn, Zc)
     if n_total is None:
         n_total = llr.shape[0]
@@ -62,36 +127,89 @@ def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="la
 
         def decode_fn(x):
             return nr_decode_ldpc_batch(x, Zc, bgn, L, "min-sum", alpha, beta, schedule)
+    pack_fn = pack_fn or pack_records
+    unpack_fn = unpack_fn or unpack_records
+    sync = torch.cuda.synchronize if llr.is_cuda else (lambda: None)
+    t0 = time.perf_counter()
     ck, st, it = decode_fn(llr)
-    info = ck[:, :K].contiguous()
-    st = st.to(torch.uint8)
-    it = it.to(torch.int32)
+    sync()
+    t1 = time.perf_counter()
+    counts = [hi - lo for lo, hi in (shard_bounds(n_total, r, world) for r in range(world))]
+    rb = record_bytes(K)
+    rec = torch.empty((max(counts + [1]), rb), dtype=torch.uint8, device=llr.device)
+    pack_fn(ck, K, st.to(torch.uint8), it.to(torch.int32), out=rec)
     if world == 1:
-        return info, st, it
-    g_info = _gather_rows(torch, dist, info, n_total, world, group)
-    g_st = _gather_rows(torch, dist, st, n_total, world, group)
-    g_it = _gather_rows(torch, dist, it, n_total, world, group)
-    if rank != dst:
-        return None
-    return g_info, g_st, g_it
+        buf, counts = rec.unsqueeze(0), [ck.shape[0]]
+    else:
+        buf = gather_record_blocks(torch, dist, rec, counts, rank, world, dst, group)
+    out = None
+    if buf is not None:
+        info = torch.empty((n_total, K), dtype=torch.int8, device=buf.device)
+        status = torch.empty((n_total,), dtype=torch.uint8, device=buf.device)
+        iters = torch.empty((n_total,), dtype=torch.int32, device=buf.device)
+        lo = 0
+        for r, c in enumerate(counts):
+            unpack_fn(buf[r], c, K, bits=info[lo:lo + c], status=status[lo:lo + c],
+                      iters=iters[lo:lo + c])
+            lo += c
+        out = (info, status, iters)
+    sync()
+    if timing is not None:
+        timing.update(decode_s=t1 - t0, gather_s=time.perf_counter() - t1,
+                      gather_bytes=rb * max(counts) * world)
+    return out
 
 
-def decode_tbs_sharded(tbs, decode_tb, group=None, dst=0):
-    """Config 5 shape: whole transport blocks round robin across ranks.  decode_tb(tb) ->
-    (crc_ok, tb_bits) runs the full per-TB chain (rate recovery, decode, CRCs) locally; the
-    (crc_ok, bits) results are gathered to rank dst as Python objects."""
+def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule="layered",
+                       T_total=None, decode_fn=None, pack_fn=None, unpack_fn=None, group=None,
+                       dst=0, timing=None):
+    """Config 5 shape: whole transport blocks round robin across ranks (every TB's CRC stays
+    rank-local), each rank running the GPU DL-SCH receive chain (sch_decode_batch: rate recovery,
+    LDPC decode, CB / TB CRCs) on its TBs; (tb_ok, tbblk) records gathered to `dst`.
+
+    llr: this rank's (T_local, G) LLR rows in round-robin order (TB rank, rank + world, ...), or
+         the full (T_total, G) batch (then the rank takes its TBs).
+    Returns on dst: (tb_ok (T_total,) uint8, tbblk (T_total, B) int8 — TB bits then CRC) in TB
+    order; None elsewhere."""
+    import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
-    mine = {i: decode_tb(tbs[i]) for i in shard_round_robin(len(tbs), rank, world)}
+    world, rank = _world(group)
+    mine_idx = None
+    if T_total is None:
+        T_total = llr.shape[0]
+        mine_idx = shard_round_robin(T_total, rank, world)
+        llr = llr[mine_idx[0]::world] if mine_idx else llr[:0]
+    if decode_fn is None:
+        from .sch import sch_decode_batch
+
+        def decode_fn(x):
+            r = sch_decode_batch(x, cfg, L, algo, alpha, beta, schedule)
+            return r.tb_ok, r.tbblk
+    pack_fn = pack_fn or pack_records
+    unpack_fn = unpack_fn or unpack_records
+    sync = torch.cuda.synchronize if llr.is_cuda else (lambda: None)
+    nb = int(cfg.B) if hasattr(cfg, "B") else int(cfg["B"])
+    t0 = time.perf_counter()
+    tb_ok, tbblk = decode_fn(llr)
+    sync()
+    t1 = time.perf_counter()
+    counts = [len(shard_round_robin(T_total, r, world)) for r in range(world)]
+    rb = record_bytes(nb, iters=False)
+    rec = torch.empty((max(counts + [1]), rb), dtype=torch.uint8, device=llr.device)
+    pack_fn(tbblk, nb, tb_ok.to(torch.uint8), None, out=rec)
     if world == 1:
-        return [mine[i] for i in range(len(tbs))]
-    parts = [None] * world
-    dist.all_gather_object(parts, {i: (bool(ok), np.asarray(b, np.int8)) for i, (ok, b) in mine.items()},
-                           group=group)
-    if rank != dst:
-        return None
-    merged = {}
-    for p in parts:
-        merged.update(p)
-    return [merged[i] for i in range(len(tbs))]
+        buf = rec.unsqueeze(0)
+    else:
+        buf = gather_record_blocks(torch, dist, rec, counts, rank, world, dst, group)
+    out = None
+    if buf is not None:
+        ok = torch.empty((T_total,), dtype=torch.uint8, device=buf.device)
+        bits = torch.empty((T_total, nb), dtype=torch.int8, device=buf.device)
+        for r, c in enumerate(counts):   # rank r holds TBs r, r + world, ...: strided rows
+            unpack_fn(buf[r], c, nb, bits=bits[r::world], status=ok[r::world])
+        out = (ok, bits)
+    sync()
+    if timing is not None:
+        timing.update(decode_s=t1 - t0, gather_s=time.perf_counter() - t1,
+                      gather_bytes=rb * max(counts) * world)
+    return out

@@ -33,6 +33,33 @@ def _free_port():
     return p
 
 
+def np_pack(bits, nbits, status=None, iters=None, out=None):
+    """Test double of shard.pack_records (the HIP kernel) for CPU tensors: same record layout."""
+    b = bits[:, :nbits].numpy().astype(np.uint8)
+    parts = [np.packbits(b, axis=1)]
+    if status is not None:
+        parts.append(status.numpy().astype(np.uint8)[:, None])
+    if iters is not None:
+        parts.append(iters.numpy().astype("<i4").view(np.uint8).reshape(-1, 4))
+    rec = np.concatenate(parts, axis=1)
+    out[:rec.shape[0], :rec.shape[1]] = torch.from_numpy(rec)
+    return out
+
+
+def np_unpack(rec, R, nbits, bits=None, status=None, iters=None):
+    """Test double of shard.unpack_records for CPU tensors."""
+    r = rec[:R].numpy()
+    nb = (nbits + 7) // 8
+    if bits is not None:
+        bits.copy_(torch.from_numpy(np.unpackbits(r[:, :nb], axis=1)[:, :nbits].astype(np.int8)))
+    o = nb
+    if status is not None:
+        status.copy_(torch.from_numpy(r[:, o].copy()))
+        o += 1
+    if iters is not None:
+        iters.copy_(torch.from_numpy(np.ascontiguousarray(r[:, o:o + 4]).view("<i4")[:, 0].copy()))
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -40,25 +67,38 @@ def _worker(rank, world, port, q):
     try:
         from oracle import ldpc_oracle as O
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded, decode_tbs_sharded
-        bg, Zc, B = 2, 12, 11
+        bg, Zc, B = 2, 13, 11                     # K = 130: not a multiple of 8 (padded bytes)
         rng = np.random.default_rng(5)           # same data on every rank (the "full batch")
         ck = rng.integers(0, 2, (B, 10 * Zc)).astype(np.int8)
         llr = O.bpsk_awgn_llr(O.encode(ck, bg), 1.0, rng).astype(np.float32)
 
         def dec(x):
             c, s, i = O.decode_layered(x.numpy(), Zc, bg, 8, 0.75, 0.0)
-            return torch.from_numpy(c), torch.from_numpy(s), torch.from_numpy(i)
+            return torch.from_numpy(c), torch.from_numpy(s.astype(np.uint8)), torch.from_numpy(i)
 
+        timing = {}
         res = decode_codeblocks_sharded(torch.from_numpy(llr), Zc, bg, 8, 0.75, 0.0,
-                                        decode_fn=dec)
-        tb = decode_tbs_sharded(list(range(5)), lambda x: (x % 2 == 0, [x, rank]))
+                                        decode_fn=dec, pack_fn=np_pack, unpack_fn=np_unpack,
+                                        timing=timing)
+        # transport blocks round robin: TB i decodes to bits i, i+1, ... and CRC flag i % 2 == 0
+        T, nb = 5, 37
+
+        def tb_dec(x):
+            idx = x[:, 0].long()
+            bits = ((idx[:, None] + torch.arange(nb)[None, :]) % 2).to(torch.int8)
+            return (idx % 2 == 0).to(torch.uint8), bits
+        tb_llr = torch.arange(T, dtype=torch.float32)[:, None].repeat(1, 3)
+        tb = decode_tbs_sharded(tb_llr, {"B": nb}, 8, decode_fn=tb_dec, pack_fn=np_pack,
+                                unpack_fn=np_unpack)
         if rank == 0:
             rc, rs, ri = O.decode_layered(llr, Zc, bg, 8, 0.75, 0.0)
+            exp_bits = (np.arange(T)[:, None] + np.arange(nb)[None, :]) % 2
             ok = (np.array_equal(res[0].numpy(), rc[:, :10 * Zc])
                   and np.array_equal(res[1].numpy().astype(bool), rs)
                   and np.array_equal(res[2].numpy(), ri)
-                  and [t[0] for t in tb] == [True, False, True, False, True]
-                  and [int(t[1][1]) for t in tb] == [i % world for i in range(5)])
+                  and tb[0].tolist() == [1, 0, 1, 0, 1]
+                  and np.array_equal(tb[1].numpy(), exp_bits)
+                  and timing["gather_bytes"] == world * 6 * (17 + 5))
             q.put(ok)
         else:
             q.put(res is None and tb is None)
