@@ -210,6 +210,26 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
                       int32_t schedule, int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok,
                       uint32_t* tb_rem, uint8_t* tb_ok, void* stream);
 
+/* ---- transport blocks with per-TB configurations (the reference configures every TB of a slot
+ * independently: nr_pdsch.py:212-281 -> DLSCHDecode at :281, nr_dlsch.py:12-74 per TB).
+ * cfgs[T] (host, each from ldpc5g_sch_config); TB t's codeblocks occupy consecutive rows of the
+ * flat workspaces, TB after TB: ck rows of K_t, dn / llr_dn rows of N_t, decoder ck rows of
+ * Nf_t = 68/52 Zc_t, status / iters / cb_crc_ok one entry per codeblock.  trblk [T][lda] (A_t
+ * bits used), g / llr [T][ldg] (E_total_t used), tbblk [T][ldb] (B_t used).
+ * sizes[7] = {ck elements, dn elements, decoder-ck elements, codeblocks, max A, max B, max E}. */
+int ldpc5g_sch_multi_sizes(const ldpc5g_sch_cfg_t* cfgs, int32_t T, int64_t* sizes);
+int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
+                            const ldpc5g_sch_cfg_t* cfgs, int32_t T, int8_t* ck, int8_t* dn,
+                            uint32_t* tb_crc, void* stream);
+/* decode: rate recovery (+ HARQ, harq_in laid out like llr_dn) -> mixed-Zc min-sum decode of all
+ * codeblocks (ldpc5g_decode_ms_mixed) -> TB reassembly + CRCs.  Asynchronous on `stream`. */
+int ldpc5g_sch_decode_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
+                            const ldpc5g_sch_cfg_t* cfgs, int32_t T, const void* harq_in,
+                            void* llr_dn, int32_t dn_dtype, int8_t* ck, uint8_t* status,
+                            int32_t* iters, int32_t L, double alpha, double beta, int32_t schedule,
+                            int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok, uint32_t* tb_rem,
+                            uint8_t* tb_ok, void* stream);
+
 /* ================================================ scrambling, modulation, soft demodulation
  * The symbol-level steps either side of the DL-SCH chain (TS 38.211 5.2.1, 5.1, 7.3.1.1-2),
  * batched over T transport blocks with one scrambling init each.  Packed bit words: bit k of

@@ -65,6 +65,16 @@ SIGNATURES = {
                                      _c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_double,
                                      _c.c_double, _c.c_int32, _c.c_void_p, _c.c_int64,
                                      _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_multi_sizes": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p]),
+    "ldpc5g_sch_encode_multi": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int64,
+                                           _c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p,
+                                           _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_decode_multi": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p,
+                                           _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                           _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                           _c.c_double, _c.c_double, _c.c_int32, _c.c_void_p,
+                                           _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                           _c.c_void_p]),
     "ldpc5g_prbs": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p, _c.c_int64,
                                _c.c_void_p]),
     "ldpc5g_scramble_modulate": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int64,

@@ -27,6 +27,8 @@ int fail(int code, const char* fmt, ...) {
 
 void clear_error() { g_err.clear(); }
 
+const char* err_text() { return g_err.c_str(); }
+
 int zc_index(int Zc) {
     for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
         if (kLdpcZcList[i] == Zc) return i;

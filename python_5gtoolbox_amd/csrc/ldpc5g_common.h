@@ -108,6 +108,7 @@ inline int dec_G(int Zc, bool layered = false) {
 // ---- host helpers (ldpc5g_capi.hip)
 int fail(int code, const char* fmt, ...);
 void clear_error();
+const char* err_text();   // message of the last fail() on this thread
 int zc_index(int Zc);
 int check_hip(hipError_t e, const char* what);
 

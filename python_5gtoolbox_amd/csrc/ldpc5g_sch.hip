@@ -260,6 +260,41 @@ struct SchDev {
     int64_t G;
 };
 
+// Per-TB geometry of a multi-configuration batch (ldpc5g_sch_*_multi): every TB has its own
+// configuration; its codeblock rows sit consecutively in the flat workspaces at these offsets.
+struct SchGeo {
+    SchDev s;
+    int64_t ck_off, dn_off, dck_off;   // elements: first row in ck (K), dn / llr_dn (N), decoder ck (Nf)
+    int32_t cb_off, dck_ld;            // first codeblock index (status, cb_ok); decoder ck row length
+};
+struct RowRef {
+    int32_t t, c;   // codeblock row -> (TB, codeblock in TB)
+};
+// Codeblock row r: one shared configuration (gv == nullptr: t = r / C, rows strided by K / N /
+// dck_ld0), or the row's TB geometry.
+struct RowGeo {
+    SchDev s;
+    int t, c, cbi;
+    int64_t ck_row, dn_row, dck_row;
+};
+__device__ __forceinline__ RowGeo row_geo(int r, const SchDev& s0, const SchGeo* gv, const RowRef* rm,
+                                          int64_t dck_ld0) {
+    RowGeo g;
+    if (!gv) {
+        g.s = s0;
+        g.t = r / s0.C, g.c = r - g.t * s0.C, g.cbi = r;
+        g.ck_row = (int64_t)r * s0.K, g.dn_row = (int64_t)r * s0.N, g.dck_row = (int64_t)r * dck_ld0;
+    } else {
+        const RowRef rr = rm[r];
+        const SchGeo& G = gv[rr.t];
+        g.s = G.s;
+        g.t = rr.t, g.c = rr.c, g.cbi = G.cb_off + rr.c;
+        g.ck_row = G.ck_off + (int64_t)rr.c * G.s.K, g.dn_row = G.dn_off + (int64_t)rr.c * G.s.N;
+        g.dck_row = G.dck_off + (int64_t)rr.c * G.dck_ld;
+    }
+    return g;
+}
+
 __device__ __forceinline__ int cb_E(const SchDev& s, int c) { return c < s.c_switch ? s.E_lo : s.E_hi; }
 __device__ __forceinline__ int64_t cb_goff(const SchDev& s, int c) {
     return (int64_t)c * s.E_lo + (int64_t)max(0, c - s.c_switch) * (s.E_hi - s.E_lo);
@@ -268,8 +303,11 @@ __device__ __forceinline__ int64_t cb_goff(const SchDev& s, int c) {
 // ------------------------------------------------------------------------------- transmit
 // TB CRC (24A / 16) of every transport block: tbcrc[t] ^= chunk contributions
 __global__ __launch_bounds__(kCrcNT) void tb_crc_kernel(const int8_t* __restrict__ trblk, int64_t lda,
-                                                        SchDev s, uint32_t* tbcrc) {
+                                                        SchDev s0, const SchGeo* __restrict__ gv,
+                                                        uint32_t* tbcrc) {
     __shared__ CrcLds S;
+    const SchDev s = gv ? gv[blockIdx.x].s : s0;
+    if ((int64_t)blockIdx.y >= crc_chunks(s.A)) return;   // multi: grid sized for the longest TB
     crc_lds_init(S, s.tbp, -1);
     const int pp[1] = {s.tbp};
     uint32_t c[1];
@@ -282,17 +320,21 @@ __global__ __launch_bounds__(kCrcNT) void tb_crc_kernel(const int8_t* __restrict
 // are copied by the CRC pass itself; the TB CRC bits that end the last codeblock are folded in
 // by linearity, crc(M1 || M2) = crc(M1) x^|M2| + crc(M2).
 __global__ __launch_bounds__(kCrcNT) void cbseg_kernel(const int8_t* __restrict__ trblk, int64_t lda,
-                                                       const uint32_t* __restrict__ tbcrc, SchDev s,
+                                                       const uint32_t* __restrict__ tbcrc, SchDev s0,
+                                                       const SchGeo* __restrict__ gv,
+                                                       const RowRef* __restrict__ rm,
                                                        int8_t* __restrict__ ck) {
     __shared__ CrcLds S;
     __shared__ uint32_t cbcrc;
     crc_lds_init(S, LDPC5G_CRC24B, -1);
-    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, 0);
+    const SchDev& s = rg.s;
+    const int t = rg.t, c = rg.c;
     const uint32_t tc = tbcrc[t];
     const int64_t base = (int64_t)c * s.cbz;
     const int nm = (int)min((int64_t)s.cbz, (int64_t)s.A - base);   // TB bits in this codeblock
     const int nt = s.cbz - nm;                                       // TB CRC bits after them
-    int8_t* out = ck + (int64_t)r * s.K;
+    int8_t* out = ck + rg.ck_row;
     const int pp[1] = {LDPC5G_CRC24B};
     uint32_t v[1];
     wg_crc_mem<1>(trblk + (int64_t)t * lda + base, out, nm, 0, pp, S, v);
@@ -316,13 +358,17 @@ __global__ __launch_bounds__(kCrcNT) void cbseg_kernel(const int8_t* __restrict_
 // thread per interleaver column i < E/Qm: it writes the Qm consecutive output bits e = i Qm + q,
 // read from the selected-bit stream at k = q E/Qm + i, so for every q a wave reads consecutive
 // bytes of dn and writes 64 Qm consecutive bytes of g.
-__global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict__ dn, SchDev s,
+__global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict__ dn, SchDev s0,
+                                                        const SchGeo* __restrict__ gv,
+                                                        const RowRef* __restrict__ rm,
                                                         int8_t* __restrict__ g, int64_t ldg) {
-    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, 0);
+    const SchDev& s = rg.s;
+    const int t = rg.t, c = rg.c;
     const int E = cb_E(s, c), EQ = E / s.Qm;
     const int i = blockIdx.y * 256 + threadIdx.x;
     if (i >= EQ) return;
-    const int8_t* src = dn + (int64_t)r * s.N;
+    const int8_t* src = dn + rg.dn_row;
     int8_t* dst = g + (int64_t)t * ldg + cb_goff(s, c) + (int64_t)i * s.Qm;
     const uint32_t size = (uint32_t)s.size, step = (uint32_t)(EQ % s.size);
     uint32_t idx = (uint32_t)(((int64_t)s.start + i) % s.size);   // circular-buffer index of k = i
@@ -359,10 +405,14 @@ __device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double
 // float64 result rounded once.
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restrict__ llr, int64_t ldg,
-                                                            SchDev s, const Tout* __restrict__ harq,
+                                                            SchDev s0, const SchGeo* __restrict__ gv,
+                                                            const RowRef* __restrict__ rm,
+                                                            const Tout* __restrict__ harq,
                                                             Tout* __restrict__ out) {
     __shared__ double red[kRrNT / 64];
-    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
+    const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, 0);
+    const SchDev& s = rg.s;
+    const int t = rg.t, c = rg.c;
     const int E = cb_E(s, c), EQ = E / s.Qm;
     const Tin* fe = llr + (int64_t)t * ldg + cb_goff(s, c);
     double m = 0.0;
@@ -375,7 +425,7 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
 #pragma unroll
     for (int w = 1; w < kRrNT / 64; ++w) m = fmax(m, red[w]);
     const double mx = m * 10.0;
-    const int64_t row = (int64_t)r * s.N;
+    const int64_t row = rg.dn_row;
     const int qE = E / s.size, rE = E - qE * s.size;   // visits of rank rr: qE + (rr < rE)
     for (int p = threadIdx.x; p < s.N; p += kRrNT) {
         double v = 0.0;
@@ -407,13 +457,17 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
 // ck[0:K_apo] when C > 1 (cb_ok = remainder 0) as crc24B(ck[0:cbz]) x^24 + crc24B(ck[cbz:K_apo]);
 // and the copy of ck[0:cbz] to the TB bits.
 __global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restrict__ ck, int64_t ldc,
-                                                          SchDev s, int8_t* __restrict__ tbblk,
+                                                          SchDev s0, const SchGeo* __restrict__ gv,
+                                                          const RowRef* __restrict__ rm,
+                                                          int8_t* __restrict__ tbblk,
                                                           int64_t ldb, uint8_t* __restrict__ cb_ok,
                                                           uint32_t* tbrem) {
     __shared__ CrcLds S;
+    const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, ldc);
+    const SchDev& s = rg.s;
+    const int t = rg.t, c = rg.c;
     crc_lds_init(S, s.tbp, LDPC5G_CRC24B);
-    const int r = blockIdx.x, t = r / s.C, c = r - t * s.C;
-    const int8_t* row = ck + (int64_t)r * ldc;
+    const int8_t* row = ck + rg.dck_row;
     const int pp[2] = {s.tbp, LDPC5G_CRC24B};
     uint32_t v[2];
     wg_crc_mem<2>(row, tbblk + (int64_t)t * ldb + (int64_t)c * s.cbz, s.cbz, 0, pp, S, v);
@@ -425,7 +479,7 @@ __global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restri
             for (int j = 0; j < 24; ++j) tail = (tail << 1) | (uint32_t)(row[s.cbz + j] & 1);
             cbr = crc_mulmod(v[1], crc_xpow(24, LDPC5G_CRC24B), 24, g) ^ crc_bits_msb(0u, tail, 24, 24, g);
         }
-        cb_ok[r] = cbr == 0u;
+        cb_ok[rg.cbi] = cbr == 0u;
         const uint32_t tbc = crc_mulmod(v[0], crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp), s.Ltb,
                                         kCrcPoly[s.tbp].g);
         if (tbc) atomicXor(&tbrem[t], tbc);
@@ -471,6 +525,71 @@ int sch_dev(const ldpc5g_sch_cfg_t* c, SchDev* s) {
 int64_t sch_total_E(const SchDev& s) {
     return (int64_t)s.c_switch * s.E_lo + (int64_t)(s.C - s.c_switch) * s.E_hi;
 }
+
+int launch_raterecover(dim3 grid, const void* llr, int llr_dtype, int64_t ldg, const SchDev& s,
+                       const SchGeo* gv, const RowRef* rm, const void* harq_in, void* llr_dn,
+                       int dn_dtype, hipStream_t st) {
+    const dim3 blk(kRrNT);
+    if (llr_dtype == LDPC5G_F32 && dn_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<float, float>), grid, blk, 0, st, (const float*)llr, ldg, s, gv, rm, (const float*)harq_in, (float*)llr_dn);
+    else if (llr_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<float, double>), grid, blk, 0, st, (const float*)llr, ldg, s, gv, rm, (const double*)harq_in, (double*)llr_dn);
+    else if (dn_dtype == LDPC5G_F32)
+        hipLaunchKernelGGL((raterecover_kernel<double, float>), grid, blk, 0, st, (const double*)llr, ldg, s, gv, rm, (const float*)harq_in, (float*)llr_dn);
+    else
+        hipLaunchKernelGGL((raterecover_kernel<double, double>), grid, blk, 0, st, (const double*)llr, ldg, s, gv, rm, (const double*)harq_in, (double*)llr_dn);
+    return check_hip(hipGetLastError(), "raterecover launch");
+}
+
+// Host side of a multi-configuration batch: validated per-TB geometry (workspace offsets in TB
+// order), the row map, and the device copy of both in a stream-ordered allocation (freed in
+// stream order by release(); asynchronous and reentrant like the mixed-Zc decode).
+struct SchMulti {
+    std::vector<SchGeo> geo;
+    std::vector<RowRef> rows;
+    int64_t ck_elems = 0, dn_elems = 0, dck_elems = 0, max_E = 0;
+    int max_A = 0, max_B = 0, max_EQ = 0;
+    void* dev = nullptr;
+    hipStream_t st = nullptr;
+
+    int build(const ldpc5g_sch_cfg_t* cfgs, int T) {
+        if (T < 0 || (T > 0 && !cfgs)) return fail(LDPC5G_ESIZE, "bad multi batch T=%d", T);
+        geo.resize(T);
+        for (int t = 0; t < T; ++t) {
+            SchGeo& G = geo[t];
+            memset(&G, 0, sizeof G);
+            if (int rc = sch_dev(&cfgs[t], &G.s)) return fail(rc, "cfgs[%d]: %s", t, err_text());
+            const int Nf = (G.s.bgn == 1 ? 68 : 52) * G.s.Zc;
+            G.ck_off = ck_elems, G.dn_off = dn_elems, G.dck_off = dck_elems;
+            G.cb_off = (int32_t)rows.size(), G.dck_ld = Nf;
+            for (int c = 0; c < G.s.C; ++c) rows.push_back(RowRef{t, c});
+            ck_elems += (int64_t)G.s.C * G.s.K, dn_elems += (int64_t)G.s.C * G.s.N;
+            dck_elems += (int64_t)G.s.C * Nf;
+            max_A = std::max(max_A, G.s.A), max_B = std::max(max_B, G.s.B);
+            max_E = std::max(max_E, sch_total_E(G.s));
+            max_EQ = std::max(max_EQ, G.s.E_hi / G.s.Qm);
+        }
+        return LDPC5G_OK;
+    }
+    int upload(hipStream_t s) {
+        st = s;
+        const size_t gb = geo.size() * sizeof(SchGeo), rb = rows.size() * sizeof(RowRef);
+        std::vector<unsigned char> host(gb + rb);
+        memcpy(host.data(), geo.data(), gb);
+        memcpy(host.data() + gb, rows.data(), rb);
+        if (int rc = check_hip(hipMallocAsync(&dev, gb + rb, st), "hipMallocAsync(sch plan)")) return rc;
+        return check_hip(hipMemcpyAsync(dev, host.data(), gb + rb, hipMemcpyHostToDevice, st), "hipMemcpyAsync(sch plan)");
+    }
+    const SchGeo* dgeo() const { return (const SchGeo*)dev; }
+    const RowRef* drows() const { return (const RowRef*)((const unsigned char*)dev + geo.size() * sizeof(SchGeo)); }
+    int release() {
+        if (!dev) return LDPC5G_OK;
+        const int rc = check_hip(hipFreeAsync(dev, st), "hipFreeAsync(sch plan)");
+        dev = nullptr;
+        return rc;
+    }
+    ~SchMulti() { release(); }
+};
 
 }  // namespace
 }  // namespace ldpc5g_impl
@@ -571,9 +690,9 @@ int ldpc5g_sch_segment(const int8_t* trblk, int64_t lda, const ldpc5g_sch_cfg_t*
     hipStream_t st = (hipStream_t)stream;
     if (int rc = check_hip(hipMemsetAsync(tb_crc, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
     hipLaunchKernelGGL(tb_crc_kernel, dim3(T, (unsigned)crc_chunks(s.A)), dim3(kCrcNT), 0, st, trblk,
-                       lda, s, tb_crc);
+                       lda, s, (const SchGeo*)nullptr, tb_crc);
     hipLaunchKernelGGL(cbseg_kernel, dim3(T * s.C), dim3(kCrcNT), 0, st, trblk, lda,
-                       (const uint32_t*)tb_crc, s, ck);
+                       (const uint32_t*)tb_crc, s, (const SchGeo*)nullptr, (const RowRef*)nullptr, ck);
     return check_hip(hipGetLastError(), "segment launch");
 }
 
@@ -590,7 +709,7 @@ int ldpc5g_sch_ratematch(const int8_t* ck, const ldpc5g_sch_cfg_t* cfg, int32_t 
     if (int rc = launch_encode(ck, dn, rows, s.bgn, s.Zc, zc_index(s.Zc), s.K, s.N, st)) return rc;
     if (s.E_hi > 0)
         hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (s.E_hi / s.Qm + 255) / 256), dim3(256), 0, st, dn,
-                           s, g, ldg);
+                           s, (const SchGeo*)nullptr, (const RowRef*)nullptr, g, ldg);
     return check_hip(hipGetLastError(), "ratematch launch");
 }
 
@@ -613,16 +732,7 @@ int ldpc5g_sch_raterecover(const void* llr, int32_t llr_dtype, int64_t ldg,
     if (T == 0) return LDPC5G_OK;
     if (!llr || !llr_dn) return fail(LDPC5G_ESIZE, "null buffer");
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid(T * s.C), blk(kRrNT);
-    if (llr_dtype == LDPC5G_F32 && dn_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<float, float>), grid, blk, 0, st, (const float*)llr, ldg, s, (const float*)harq_in, (float*)llr_dn);
-    else if (llr_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<float, double>), grid, blk, 0, st, (const float*)llr, ldg, s, (const double*)harq_in, (double*)llr_dn);
-    else if (dn_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<double, float>), grid, blk, 0, st, (const double*)llr, ldg, s, (const float*)harq_in, (float*)llr_dn);
-    else
-        hipLaunchKernelGGL((raterecover_kernel<double, double>), grid, blk, 0, st, (const double*)llr, ldg, s, (const double*)harq_in, (double*)llr_dn);
-    return check_hip(hipGetLastError(), "raterecover launch");
+    return launch_raterecover(dim3(T * s.C), llr, llr_dtype, ldg, s, nullptr, nullptr, harq_in, llr_dn, dn_dtype, st);
 }
 
 int ldpc5g_sch_tb_check(const int8_t* ck, int64_t ldc, const ldpc5g_sch_cfg_t* cfg, int32_t T,
@@ -637,8 +747,8 @@ int ldpc5g_sch_tb_check(const int8_t* ck, int64_t ldc, const ldpc5g_sch_cfg_t* c
     if (!ck || !tbblk || !cb_crc_ok || !tb_rem || !tb_ok) return fail(LDPC5G_ESIZE, "null buffer");
     hipStream_t st = (hipStream_t)stream;
     if (int rc = check_hip(hipMemsetAsync(tb_rem, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
-    hipLaunchKernelGGL(tb_check_kernel, dim3(T * s.C), dim3(kCrcNT), 0, st, ck, ldc, s, tbblk, ldb,
-                       cb_crc_ok, tb_rem);
+    hipLaunchKernelGGL(tb_check_kernel, dim3(T * s.C), dim3(kCrcNT), 0, st, ck, ldc, s,
+                       (const SchGeo*)nullptr, (const RowRef*)nullptr, tbblk, ldb, cb_crc_ok, tb_rem);
     hipLaunchKernelGGL(tb_ok_kernel, dim3((T + 255) / 256), dim3(256), 0, st, (const uint32_t*)tb_rem,
                        tb_ok, (int)T);
     return check_hip(hipGetLastError(), "tb_check launch");
@@ -656,6 +766,96 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
                                   alpha, beta, schedule, 0, cfg->N, Nf, stream))
         return rc;
     return ldpc5g_sch_tb_check(ck, Nf, cfg, T, tbblk, ldb, cb_crc_ok, tb_rem, tb_ok, stream);
+}
+
+int ldpc5g_sch_multi_sizes(const ldpc5g_sch_cfg_t* cfgs, int32_t T, int64_t* sizes) {
+    clear_error();
+    if (!sizes) return fail(LDPC5G_ESIZE, "null sizes");
+    SchMulti m;
+    if (int rc = m.build(cfgs, T)) return rc;
+    sizes[0] = m.ck_elems, sizes[1] = m.dn_elems, sizes[2] = m.dck_elems, sizes[3] = (int64_t)m.rows.size();
+    sizes[4] = m.max_A, sizes[5] = m.max_B, sizes[6] = m.max_E;
+    return LDPC5G_OK;
+}
+
+int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
+                            const ldpc5g_sch_cfg_t* cfgs, int32_t T, int8_t* ck, int8_t* dn,
+                            uint32_t* tb_crc, void* stream) {
+    clear_error();
+    SchMulti m;
+    if (int rc = m.build(cfgs, T)) return rc;
+    if (T > 1 && (lda < m.max_A || ldg < m.max_E))
+        return fail(LDPC5G_ESIZE, "bad strides lda=%lld ldg=%lld (max A %d, max E %lld)", (long long)lda, (long long)ldg, m.max_A, (long long)m.max_E);
+    if (T == 0) return LDPC5G_OK;
+    if (!trblk || !g || !ck || !dn || !tb_crc) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = m.upload(st)) return rc;
+    const SchDev s0{};
+    const int rows = (int)m.rows.size();
+    if (int rc = check_hip(hipMemsetAsync(tb_crc, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
+    hipLaunchKernelGGL(tb_crc_kernel, dim3(T, (unsigned)crc_chunks(m.max_A)), dim3(kCrcNT), 0, st, trblk,
+                       lda, s0, m.dgeo(), tb_crc);
+    hipLaunchKernelGGL(cbseg_kernel, dim3(rows), dim3(kCrcNT), 0, st, trblk, lda, (const uint32_t*)tb_crc,
+                       s0, m.dgeo(), m.drows(), ck);
+    if (int rc = check_hip(hipGetLastError(), "segment launch")) return rc;
+    // encoder: one launch per run of consecutive TBs with the same (bgn, Zc) (their rows are
+    // contiguous with one stride)
+    for (int t0 = 0; t0 < T;) {
+        const SchDev& a = m.geo[t0].s;
+        int t1 = t0 + 1, n = a.C;
+        while (t1 < T && m.geo[t1].s.bgn == a.bgn && m.geo[t1].s.Zc == a.Zc) n += m.geo[t1++].s.C;
+        if (int rc = launch_encode(ck + m.geo[t0].ck_off, dn + m.geo[t0].dn_off, n, a.bgn, a.Zc,
+                                   zc_index(a.Zc), a.K, a.N, st))
+            return rc;
+        t0 = t1;
+    }
+    if (m.max_EQ > 0)
+        hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (m.max_EQ + 255) / 256), dim3(256), 0, st, dn, s0,
+                           m.dgeo(), m.drows(), g, ldg);
+    if (int rc = check_hip(hipGetLastError(), "ratematch launch")) return rc;
+    return m.release();
+}
+
+int ldpc5g_sch_decode_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
+                            const ldpc5g_sch_cfg_t* cfgs, int32_t T, const void* harq_in,
+                            void* llr_dn, int32_t dn_dtype, int8_t* ck, uint8_t* status,
+                            int32_t* iters, int32_t L, double alpha, double beta, int32_t schedule,
+                            int8_t* tbblk, int64_t ldb, uint8_t* cb_crc_ok, uint32_t* tb_rem,
+                            uint8_t* tb_ok, void* stream) {
+    clear_error();
+    SchMulti m;
+    if (int rc = m.build(cfgs, T)) return rc;
+    if ((llr_dtype != LDPC5G_F32 && llr_dtype != LDPC5G_F64) || (dn_dtype != LDPC5G_F32 && dn_dtype != LDPC5G_F64))
+        return fail(LDPC5G_ESIZE, "bad dtype");
+    if (T > 1 && (ldg < m.max_E || ldb < m.max_B))
+        return fail(LDPC5G_ESIZE, "bad strides ldg=%lld ldb=%lld (max E %lld, max B %d)", (long long)ldg, (long long)ldb, (long long)m.max_E, m.max_B);
+    if (T == 0) return LDPC5G_OK;
+    if (!llr || !llr_dn || !ck || !status || !iters || !tbblk || !cb_crc_ok || !tb_rem || !tb_ok)
+        return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = m.upload(st)) return rc;
+    const SchDev s0{};
+    const int rows = (int)m.rows.size();
+    if (int rc = launch_raterecover(dim3(rows), llr, llr_dtype, ldg, s0, m.dgeo(), m.drows(), harq_in, llr_dn,
+                                    dn_dtype, st))
+        return rc;
+    // every codeblock with its own (bgn, Zc): the mixed-Zc decoder (<= 2 launches)
+    std::vector<ldpc5g_cb_desc_t> desc(rows);
+    for (int r = 0; r < rows; ++r) {
+        const SchGeo& G = m.geo[m.rows[r].t];
+        const int c = m.rows[r].c;
+        desc[r].bgn = G.s.bgn, desc[r].Zc = G.s.Zc;
+        desc[r].llr_off = G.dn_off + (int64_t)c * G.s.N, desc[r].ck_off = G.dck_off + (int64_t)c * G.dck_ld;
+    }
+    if (int rc = ldpc5g_decode_ms_mixed(desc.data(), rows, llr_dn, dn_dtype, ck, status, iters, L, alpha, beta,
+                                        schedule, 0, stream))
+        return rc;
+    if (int rc = check_hip(hipMemsetAsync(tb_rem, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
+    hipLaunchKernelGGL(tb_check_kernel, dim3(rows), dim3(kCrcNT), 0, st, (const int8_t*)ck, (int64_t)0, s0,
+                       m.dgeo(), m.drows(), tbblk, ldb, cb_crc_ok, tb_rem);
+    hipLaunchKernelGGL(tb_ok_kernel, dim3((T + 255) / 256), dim3(256), 0, st, (const uint32_t*)tb_rem, tb_ok, (int)T);
+    if (int rc = check_hip(hipGetLastError(), "tb_check launch")) return rc;
+    return m.release();
 }
 
 }  // extern "C"

@@ -215,3 +215,82 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
         sch_tb_check_batch(ws.dec_ck, cfg, T, ws)
     return SchDecodeResult(ws.tb_ok, ws.tbblk, llr_dn, ws.dec_ck, ws.status, ws.iters, ws.cb_ok,
                            ws.tb_rem)
+
+
+# ------------------------------------------------------------ per-TB configurations (multi)
+SchMultiResult = namedtuple(
+    "SchMultiResult", "tb_ok tbblk llr_dn ck status iters cb_crc_ok tb_rem rows")
+
+
+def multi_layout(cfgs):
+    """Workspace geometry of a batch whose transport blocks each have their own configuration
+    (ldpc5g_sch_multi_sizes): dict(ck, dn, dck, ncb, max_A, max_B, max_E) plus `rows`: per TB
+    (first codeblock, C, dn element offset, N, decoder-ck offset, Nf) in workspace order."""
+    T = len(cfgs)
+    arr = (_lib.SchCfg * max(T, 1))(*cfgs)
+    sizes = (_lib.ctypes.c_int64 * 7)()
+    _lib.check(_lib.lib().ldpc5g_sch_multi_sizes(arr, T, sizes))
+    rows, cb, dn, dck = [], 0, 0, 0
+    for c in cfgs:
+        nf = (68 if c.bgn == 1 else 52) * c.Zc
+        rows.append((cb, c.C, dn, c.N, dck, nf))
+        cb, dn, dck = cb + c.C, dn + c.C * c.N, dck + c.C * nf
+    return dict(ck=sizes[0], dn=sizes[1], dck=sizes[2], ncb=sizes[3], max_A=sizes[4],
+                max_B=sizes[5], max_E=sizes[6], rows=rows, arr=arr)
+
+
+def sch_encode_multi(trblk, cfgs):
+    """DLSCHEncode / UL-SCH encode of T transport blocks with per-TB configurations in one call
+    (ldpc5g_sch_encode_multi).  trblk: (T, >= max A) int8 device tensor (TB t uses A_t bits).
+    Returns g (T, max E_total) int8 (TB t's first E_total_t entries valid)."""
+    t = _lib.require_gpu()
+    T = len(cfgs)
+    lay = multi_layout(cfgs)
+    assert trblk.dim() == 2 and trblk.shape[0] == T and trblk.dtype == t.int8 and trblk.stride(1) == 1
+    assert trblk.shape[1] >= lay["max_A"]
+    dev = trblk.device
+    g = t.empty((T, max(lay["max_E"], 1)), dtype=t.int8, device=dev)
+    ck = t.empty((max(lay["ck"], 1),), dtype=t.int8, device=dev)
+    dn = t.empty((max(lay["dn"], 1),), dtype=t.int8, device=dev)
+    crc = t.empty((max(T, 1),), dtype=t.int32, device=dev)
+    with t.cuda.device(dev):
+        _lib.check(_lib.lib().ldpc5g_sch_encode_multi(
+            _lib.ptr(trblk), trblk.stride(0), _lib.ptr(g), g.stride(0), lay["arr"], T,
+            _lib.ptr(ck), _lib.ptr(dn), _lib.ptr(crc), _lib.stream_ptr(dev)))
+    return g
+
+
+def sch_decode_multi(llr, cfgs, L, alpha=1.0, beta=0.0, schedule="flooding", harq_in=None,
+                     dn_dtype=None):
+    """DLSCHDecode / ULSCH_decoding of T transport blocks with per-TB configurations in one call
+    (ldpc5g_sch_decode_multi): rate recovery, every codeblock decoded by the mixed-Zc decoder,
+    TB reassembly and CRCs.  llr: (T, >= max E_total) float32/64 device tensor.
+    Returns SchMultiResult(tb_ok (T,), tbblk (T, max B) — TB t's first B_t bits, llr_dn flat
+    (the HARQ buffers new_LLr_dns of every TB, rows[t] locates them), ck flat, status, iters,
+    cb_crc_ok (per codeblock), tb_rem, rows)."""
+    t = _lib.require_gpu()
+    T = len(cfgs)
+    lay = multi_layout(cfgs)
+    assert llr.dim() == 2 and llr.shape[0] == T and llr.stride(1) == 1 and llr.shape[1] >= lay["max_E"]
+    dn_dtype = dn_dtype or (t.float32 if schedule == "layered" else llr.dtype)
+    dev = llr.device
+    llr_dn = t.empty((max(lay["dn"], 1),), dtype=dn_dtype, device=dev)
+    if harq_in is not None:
+        assert harq_in.dtype == dn_dtype and harq_in.numel() >= lay["dn"] and harq_in.is_contiguous()
+    ck = t.empty((max(lay["dck"], 1),), dtype=t.int8, device=dev)
+    n = max(lay["ncb"], 1)
+    status = t.empty((n,), dtype=t.uint8, device=dev)
+    iters = t.empty((n,), dtype=t.int32, device=dev)
+    cb_ok = t.empty((n,), dtype=t.uint8, device=dev)
+    tbblk = t.empty((T, max(lay["max_B"], 1)), dtype=t.int8, device=dev)
+    tb_rem = t.empty((max(T, 1),), dtype=t.int32, device=dev)
+    tb_ok = t.empty((max(T, 1),), dtype=t.uint8, device=dev)
+    sched = {"flooding": _lib.FLOODING, "layered": _lib.LAYERED}[schedule]
+    with t.cuda.device(dev):
+        _lib.check(_lib.lib().ldpc5g_sch_decode_multi(
+            _lib.ptr(llr), _dtype_id(t, llr.dtype), llr.stride(0), lay["arr"], T,
+            _lib.ptr(harq_in) if harq_in is not None else None, _lib.ptr(llr_dn),
+            _dtype_id(t, dn_dtype), _lib.ptr(ck), _lib.ptr(status), _lib.ptr(iters), int(L),
+            float(alpha), float(beta), sched, _lib.ptr(tbblk), tbblk.stride(0), _lib.ptr(cb_ok),
+            _lib.ptr(tb_rem), _lib.ptr(tb_ok), _lib.stream_ptr(dev)))
+    return SchMultiResult(tb_ok[:T], tbblk, llr_dn, ck, status, iters, cb_ok, tb_rem, lay["rows"])

@@ -243,3 +243,95 @@ def test_config5_tb_stream_round_trip(torch, sch, gold):
     r = sch.sch_decode_batch(llr.contiguous(), cfg, 8, "min-sum", 0.75, 0.0, "layered")
     assert r.tb_ok.cpu().numpy().all() and r.cb_crc_ok.cpu().numpy().all()
     assert torch.equal(r.tbblk[:, :cs["TBS"]], xt)
+
+
+# ------------------------------------------------------------ per-TB configurations (multi)
+def _cfg_of(sch, cs, rv=None):
+    lbrm = cs["LBRM"] if cs["kind"] != "ul" else 0
+    return sch.sch_config(cs["TBS"], cs["Qm"], cs["R"], cs["NL"], cs["rv"] if rv is None else rv,
+                          lbrm, cs["G"])
+
+
+def test_sch_multi_encode_golden(torch, sch, gold):
+    """Five transport blocks with five different configurations (DL with limited buffer, UL with
+    Ncb = N, QPSK..256QAM, 1..4 layers, the config-5 TB of 129 codeblocks) in ONE
+    ldpc5g_sch_encode_multi call == the reference's DLSCHEncode / ULSCH encode per TB."""
+    cases, z = gold
+    idx = [0, 2, 3, 4, 5]
+    cfgs = [_cfg_of(sch, cases[n]) for n in idx]
+    Amax = max(cases[n]["TBS"] for n in idx)
+    tb = np.zeros((len(idx), Amax), np.int8)
+    for t, n in enumerate(idx):
+        tb[t, :cases[n]["TBS"]] = _bits(z, f"trblk{n}", cases[n]["TBS"])
+    g = sch.sch_encode_multi(torch.from_numpy(tb).cuda(), cfgs).cpu().numpy()
+    for t, n in enumerate(idx):
+        assert cfgs[t].E_total == cases[n]["G"]
+        assert np.array_equal(g[t, :cfgs[t].E_total], _bits(z, f"g{n}", cases[n]["G"])), n
+
+
+def test_sch_multi_decode_golden(torch, sch, gold):
+    """Four transport blocks with different configurations (two DL, two UL; different Zc and
+    base graphs) in ONE ldpc5g_sch_decode_multi call, float64 flooding = the reference's
+    DLSCHDecode / ULSCH_decoding per TB: crc_ok, TB bits and the HARQ buffer new_LLr_dns (sha256)
+    bit-exact; then the two DL TBs retransmitted (rv 2) with HARQ combining in one call."""
+    cases, z = gold
+    idx = [0, 2, 3, 4]
+    cfgs = [_cfg_of(sch, cases[n]) for n in idx]
+    Emax = max(c.E_total for c in cfgs)
+    llr = np.zeros((len(idx), Emax), np.float64)
+    for t, n in enumerate(idx):
+        llr[t, :cfgs[t].E_total] = z[f"llr{n}"].astype(np.float64)
+    r = sch.sch_decode_multi(torch.from_numpy(llr).cuda(), cfgs, DEC["L"], DEC["alpha"],
+                             DEC["beta"], "flooding")
+    ok, tbblk, dn = r.tb_ok.cpu().numpy(), r.tbblk.cpu().numpy(), r.llr_dn.cpu().numpy()
+    assert len({(c.bgn, c.Zc) for c in cfgs}) > 1
+    for t, n in enumerate(idx):
+        cs = cases[n]
+        assert bool(ok[t]) == cs["ok"], n
+        assert np.array_equal(tbblk[t, :cs["TBS"]], _bits(z, f"tbblk{n}", cs["TBS"])), n
+        cb0, C, off, N, _, _ = r.rows[t]
+        new = dn[off:off + C * N].reshape(C, N)
+        assert list(new.shape) == cs["new_shape"] and _sha(new) == cs["new_sha"], n
+    # HARQ retransmission of the DL TBs: rv 2, combined with their first-pass buffers
+    dl = [0, 1]
+    cfg1 = [cfgs[t] for t in dl]
+    r1 = sch.sch_decode_multi(torch.from_numpy(llr[dl]).cuda(), cfg1, DEC["L"], DEC["alpha"],
+                              DEC["beta"], "flooding")
+    cfg2 = [_cfg_of(sch, cases[idx[t]], rv=2) for t in dl]
+    E2 = max(c.E_total for c in cfg2)
+    llr2 = np.zeros((len(dl), E2), np.float64)
+    for k, t in enumerate(dl):
+        llr2[k, :cfg2[k].E_total] = z[f"llr2_{idx[t]}"].astype(np.float64)
+    r2 = sch.sch_decode_multi(torch.from_numpy(llr2).cuda(), cfg2, DEC["L"], DEC["alpha"],
+                              DEC["beta"], "flooding", harq_in=r1.llr_dn)
+    ok2, tb2, dn2 = r2.tb_ok.cpu().numpy(), r2.tbblk.cpu().numpy(), r2.llr_dn.cpu().numpy()
+    for k, t in enumerate(dl):
+        cs = cases[idx[t]]
+        assert bool(ok2[k]) == cs["ok2"], idx[t]
+        assert np.array_equal(tb2[k, :cs["TBS"]], _bits(z, f"tbblk2_{idx[t]}", cs["TBS"])), idx[t]
+        cb0, C, off, N, _, _ = r2.rows[k]
+        assert _sha(dn2[off:off + C * N].reshape(C, N)) == cs["new2_sha"], idx[t]
+
+
+def test_sch_multi_layered_matches_single_config_batches(torch, sch):
+    """Layered float32 through the multi chain == the single-configuration chain run per
+    configuration (same codeblocks, same kernels' arithmetic): tb_ok, TB bits, iterations."""
+    rng = np.random.default_rng(9)
+    specs = [(24000, 4, 700, 1, 0, 60000, 30000), (3000, 2, 300, 1, 1, 10000, 9000),
+             (60000, 8, 900, 2, 2, 60000, 64000)]
+    cfgs = [sch.sch_config(*a) for a in specs]
+    T = len(cfgs)
+    Emax = max(c.E_total for c in cfgs)
+    llr = np.zeros((T, Emax), np.float32)
+    for t, (a, c) in enumerate(zip(specs, cfgs)):
+        tb = rng.integers(0, 2, (1, a[0])).astype(np.int8)
+        g = sch.sch_encode_batch(torch.from_numpy(tb).cuda(), c).cpu().numpy()[0]
+        llr[t, :c.E_total] = (1 - 2 * g.astype(np.float32)) * 4 + rng.normal(0, 1.2, c.E_total)
+    r = sch.sch_decode_multi(torch.from_numpy(llr).cuda(), cfgs, 8, 0.75, 0.0, "layered")
+    for t, c in enumerate(cfgs):
+        one = sch.sch_decode_batch(torch.from_numpy(llr[t:t + 1, :c.E_total].copy()).cuda(), c, 8,
+                                   "min-sum", 0.75, 0.0, "layered")
+        assert int(r.tb_ok[t]) == int(one.tb_ok[0])
+        assert torch.equal(r.tbblk[t, :c.B], one.tbblk[0, :c.B])
+        cb0, C, _, _, _, _ = r.rows[t]
+        assert torch.equal(r.iters[cb0:cb0 + C], one.iters[:C])
