@@ -96,9 +96,62 @@ def build(force=False, verbose=True, csrc=None, out=None):
     return lib_path
 
 
+ASAN_LIB = os.path.join(ROOT, "build", "asan", "libldpc5g.so")
+
+
+def asan_runtime():
+    """The clang ASan runtime a non-instrumented interpreter must preload to load ASAN_LIB."""
+    res = subprocess.run([HIPCC, "--print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True,
+                         text=True)
+    p = res.stdout.strip()
+    if not os.path.isabs(p):   # older drivers: search the resource directory
+        rd = subprocess.run([HIPCC, "-print-resource-dir"], capture_output=True, text=True).stdout.strip()
+        p = os.path.join(rd, "lib", "linux", "libclang_rt.asan-x86_64.so")
+    return p
+
+
+def build_asan(force=False, verbose=False):
+    """Host-code sanitizer build: every TU's HOST code compiled with
+    AddressSanitizer + UndefinedBehaviorSanitizer (-Xarch_host: the device code is the normal
+    gfx950 build), into build/asan/libldpc5g.so.  It backs the CPU suite's
+    validation / plan-building / configuration tests (tests/test_asan_host.py), which exercise
+    exactly the C-ABI host code: argument checks, ldpc5g_sch_config, the mixed-Zc and per-TB plans."""
+    out_dir = os.path.dirname(ASAN_LIB)
+    if not force and os.path.exists(ASAN_LIB) and \
+            all(os.path.getmtime(d) <= os.path.getmtime(ASAN_LIB) for d in deps()):
+        return ASAN_LIB
+    os.makedirs(out_dir, exist_ok=True)
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer"]
+    base = list(FLAGS)
+
+    def one(src):
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *base, *san, "-c", src, "-o", obj]
+        if os.path.basename(src) in NO_SLP:
+            cmd.insert(1, "-fno-slp-vectorize")
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+    srcs = sources()
+    with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
+        objs = list(ex.map(one, srcs))
+    link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Xarch_host", "-fsanitize=address", "-Xarch_host",
+            "-fsanitize=undefined", "-shared-libasan", *objs, "-o", ASAN_LIB + ".tmp"]
+    if verbose:
+        print(" ".join(link), flush=True)
+    subprocess.run(link, check=True)
+    os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
+    return ASAN_LIB
+
+
 def _arg(name):
     return sys.argv[sys.argv.index(name) + 1] if name in sys.argv else None
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, csrc=_arg("--csrc"), out=_arg("--out"))
+    if "--asan" in sys.argv:
+        print(build_asan(force="--force" in sys.argv, verbose=True))
+    else:
+        build(force="--force" in sys.argv, csrc=_arg("--csrc"), out=_arg("--out"))

@@ -167,3 +167,39 @@ def test_product_fails_loudly_without_gpu():
         nr_ldpc_encode.encode_ldpc(np.zeros(80, np.int8), 2)
     with pytest.raises(_lib.LdpcLibError):
         nr_ldpc_decode.nr_decode_ldpc(np.zeros(400), 8, 2, 8)
+
+
+def test_mixed_plan_built_on_host():
+    """ldpc5g_mixed_plan is pure host code: sizing call, then the plan (header: schedule, BG1 / BG2
+    workgroups, codeblock refs) for 5 BG1 Zc=384 + 3 BG2 Zc=12 codeblocks, layered (G = 2 and
+    64 per workgroup) and flooding (G = 1 and 32)."""
+    lib = _lib.lib()
+    d = (_lib.CbDesc * 8)()
+    for k in range(8):
+        d[k].bgn, d[k].Zc = (1, 384) if k < 5 else (2, 12)
+        d[k].llr_off, d[k].ck_off = 1000 * k, 2000 * k
+    for sched, nw1, nw2 in ((_lib.LAYERED, 3, 1), (_lib.FLOODING, 5, 1)):
+        n = lib.ldpc5g_mixed_plan(d, 8, sched, None, 0)
+        assert n == 24 + 16 * (nw1 + nw2) + 24 * 8
+        buf = (ctypes.c_ubyte * n)()
+        assert lib.ldpc5g_mixed_plan(d, 8, sched, buf, n) == n
+        hdr = np.frombuffer(bytes(buf)[:24], np.int32)
+        assert hdr[1] == sched and hdr[2] == nw1 and hdr[3] == nw2 and hdr[4] == 8
+    d[3].Zc = 383
+    assert lib.ldpc5g_mixed_plan(d, 8, _lib.LAYERED, None, 0) == _lib.EZC
+    assert lib.ldpc5g_decode_ms_mixed_plan(None, None, None, 1, None, None, None, 8, 1.0, 0.0,
+                                           _lib.LAYERED, 0, None) == _lib.ESIZE
+
+
+@pytest.mark.parametrize("call,code", [
+    (lambda l: l.ldpc5g_pack_records(None, 10, 2, 10, None, None, None, 1, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_unpack_records(None, 8, 2, 10, None, 10, None, None, 0, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_pack_records(None, 10, 0, 10, None, None, None, 2, None), 0),
+    (lambda l: l.ldpc5g_scramble_modulate(None, 10, None, 0, 1, 10, 3, None, 10, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_demod_descramble(None, 1, 10, None, 10, None, 0, 1, 10, 2, None, 0, 20,
+                                         None), _lib.ESIZE),   # float64 LLRs need BPSK + c128
+    (lambda l: l.ldpc5g_demod_descramble(None, 0, 10, None, 10, None, 0, 1, 10, 1, None, 0, 10,
+                                         None), _lib.ESIZE),   # null buffers
+])
+def test_pack_and_phy_validation_without_gpu(call, code):
+    assert call(_lib.lib()) == code

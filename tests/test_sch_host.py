@@ -132,3 +132,22 @@ def test_oracle_sch_chain_matches_reference_sch_golden():
         ok, blk, _ = O.sch_tb_check(ck, p)
         assert ok == cs["ok"]
         assert np.array_equal(blk, np.unpackbits(z[f"tbblk{n}"])[:A].astype(np.int8))
+
+
+def test_sch_multi_sizes_host():
+    """ldpc5g_sch_multi_sizes (host code) == the Python layout of a per-TB-configuration batch,
+    and a bad configuration anywhere in the list is reported with its index."""
+    from python_5gtoolbox_amd.sch import multi_layout
+    cfgs = [sch_config(12000, 4, 517, 1, 0, 30000, 25000), sch_config(1800, 2, 308, 1, 0, 40000, 6000),
+            sch_config(1081512, 8, 948, 4, 0, 1081512, 1153152)]
+    lay = multi_layout(cfgs)
+    assert lay["ncb"] == sum(c.C for c in cfgs)
+    assert lay["ck"] == sum(c.C * c.K for c in cfgs) and lay["dn"] == sum(c.C * c.N for c in cfgs)
+    assert lay["max_A"] == 1081512 and lay["max_E"] == max(c.E_total for c in cfgs)
+    assert [r[0] for r in lay["rows"]] == [0, cfgs[0].C, cfgs[0].C + cfgs[1].C]
+    bad = _lib.SchCfg.from_buffer_copy(cfgs[1])
+    bad.K_apo += 1
+    arr = (_lib.SchCfg * 3)(cfgs[0], bad, cfgs[2])
+    sizes = (ctypes.c_int64 * 7)()
+    assert _lib.lib().ldpc5g_sch_multi_sizes(arr, 3, sizes) == _lib.ESIZE
+    assert b"cfgs[1]" in _lib.lib().ldpc5g_last_error()
