@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip 
 # rocprofv3 PMC summary of this code version (tools/gpu_round.sh pmc step -> tools/pmc_summary.py),
 # committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
-DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true>",
+DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false>",
               "flooding": "void ldpc_dec_kernel<1, float, false>"}
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
