@@ -1,0 +1,532 @@
+// ldpc5g_dec_flood.h — flooding min-sum decoder (py5gphy/ldpc/nr_ldpc_decode.py:51-143 with
+// _min_sum_process :178-227), float64 (bit-identical to the reference) and float32.
+//
+// One iteration of the reference computes every check-to-variable message Lr from Lq = LQ_old - Lr_old
+// (:117-123), then LQ_new = LLRin + Lr.sum(axis=0) (:126), a row-ascending sum per column.  The
+// kernel splits it the same way:
+//   phase A  every base row reads LQ_old (LDS, read-only in this phase, no barrier between rows),
+//            forms q = LQ_old - r_old edge by edge and keeps only the new compressed row state
+//            (nA = alpha*max(min1-beta,0), nB = ... min2, per-edge signs, argmin);  the syndrome
+//            of the hard decisions of LQ_old (:107-114) falls out of the same reads;
+//   phase B  the messages r are rebuilt from the new state and summed into the SAME LDS array
+//            (LQ_old is dead now) in row-ascending order, one barrier per group of column-disjoint
+//            rows; the first row of each column writes 0 + r instead of adding;
+//   then     LQ = LLR + sum for the thread's own entries.
+// So one f64 array of the Kb+4 core columns (80 KB at Zc = 384) is the whole LDS image of LQ, and
+// the remaining LDS holds the state of the first rows.  Every thread slot (z, codeblock) has two
+// threads, one per half of the 768-thread workgroup (6 waves each, 3 waves per SIMD): the base rows
+// are split between the halves (phase-A edge counts balanced, the rows of a multi-row group on
+// different halves so phase B stays balanced), so each thread holds the state of ~half the rows
+// in VGPRs.  Rows whose state lives in LDS are summed by both halves (alternate edges) in phase B.
+#pragma once
+#include "ldpc5g_dec_body.h"
+
+namespace ldpc5g_impl {
+namespace {
+
+constexpr int kFloodThreads = 2 * kDecThreads;   // two halves of 384 slots
+constexpr size_t kLdsPerCU = 160 * 1024;
+#ifndef LDPC5G_FLOOD_CHUNK
+#define LDPC5G_FLOOD_CHUNK 6
+#endif
+constexpr int kSchedChunk = LDPC5G_FLOOD_CHUNK;
+
+template <int BG, typename T>
+struct FloodPlan {
+    int nls = 0;          // rows 0..nls-1 keep their state in LDS
+    int owner[64] = {};   // half that runs phase A of row i (and phase B of a VGPR row)
+    int slot[64] = {};    // VGPR state slot of row i in its owner half (-1: LDS row)
+    int nslot = 0;
+    int pw[64] = {};      // VGPR sign word of row i: rows of degree <= 12 share a word (16-bit fields)
+    int ph[64] = {};      // 0: whole word (negs | idx << 24), 1: low field, 2: high field (negs | idx << 12)
+    int npw = 0;
+    int first_row[32] = {};   // lowest base row of core column j (writes 0 + r in phase B)
+    static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
+    constexpr FloodPlan() {
+        using P = BGT<BG>;
+        constexpr int CS = kDecThreads;
+        const auto& G = kGroups<BG>;
+        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4 + 2 * CS * 4;
+        const int fit = (int)((kLdsPerCU - fixed) / (CS * (2 * sizeof(T) + 4)));
+        int lead = 0;   // leading single-row groups: their phase B is split only if in LDS
+        while (lead < G.n && G.start[lead + 1] - G.start[lead] == 1 && G.start[lead] == lead) ++lead;
+        nls = fit < lead ? fit : lead;
+        int load[2] = {0, 0};
+        bool done[64] = {};
+        for (int g = 0; g < G.n; ++g) {
+            if (G.start[g + 1] - G.start[g] < 2) continue;
+            int gl[2] = {0, 0};
+            for (;;) {
+                int best = -1;
+                for (int i = G.start[g]; i < G.start[g + 1]; ++i)
+                    if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
+                if (best < 0) break;
+                const int h = gl[0] != gl[1] ? (gl[0] < gl[1] ? 0 : 1) : (load[0] <= load[1] ? 0 : 1);
+                owner[best] = h, gl[h] += deg(best), load[h] += deg(best), done[best] = true;
+            }
+        }
+        for (;;) {
+            int best = -1;
+            for (int i = 0; i < P::MB; ++i)
+                if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
+            if (best < 0) break;
+            const int h = load[0] <= load[1] ? 0 : 1;
+            owner[best] = h, load[h] += deg(best), done[best] = true;
+        }
+        int ns[2] = {0, 0};
+        for (int i = 0; i < P::MB; ++i) slot[i] = i < nls ? -1 : ns[owner[i]]++;
+        nslot = ns[0] > ns[1] ? ns[0] : ns[1];
+        for (int hh = 0; hh < 2; ++hh) {
+            int n = 0, open = -1;
+            for (int i = nls; i < P::MB; ++i) {
+                if (owner[i] != hh) continue;
+                if (deg(i) > 12) {
+                    pw[i] = n++, ph[i] = 0;
+                } else if (open >= 0) {
+                    pw[i] = open, ph[i] = 2, open = -1;
+                } else {
+                    open = n, pw[i] = n++, ph[i] = 1;
+                }
+            }
+            npw = npw > n ? npw : n;
+        }
+        for (int j = 0; j < P::KC; ++j) {
+            first_row[j] = -1;
+            for (int i = 0; i < P::MB && first_row[j] < 0; ++i)
+                for (int e = P::RS[i]; e < P::RS[i + 1]; ++e)
+                    if (P::COL[e] == j) first_row[j] = i;
+        }
+    }
+};
+template <int BG, typename T>
+constexpr FloodPlan<BG, T> kFloodPlan{};
+
+template <int BG, typename T>
+constexpr size_t flood_lds_bytes_t() {
+    constexpr int CS = kDecThreads;
+    return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T>.nls * CS * (2 * sizeof(T) + 4) +
+           (2 * kMaxG + 4) * 4 + 2 * CS * 4;
+}
+
+// x with its sign flipped by bit 31 of u (all-VGPR v_bitop3: x ^ (u & mv), mv = 0x80000000)
+__device__ __forceinline__ float xsign_v(float x, uint32_t u, uint32_t mv) {
+    return __uint_as_float(__builtin_amdgcn_bitop3_b32(u, __float_as_uint(x), mv, 0x6c));
+}
+__device__ __forceinline__ double xsign_v(double x, uint32_t u, uint32_t mv) {
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32(u, (uint32_t)__double2hiint(x), mv, 0x6c);
+    return __hiloint2double((int)hi, __double2loint(x));
+}
+template <int BG>
+__device__ __forceinline__ const uint32_t* shift_row(int zi) {
+    if constexpr (BG == 1) return kBG1ShiftMod[zi];
+    else return kBG2ShiftMod[zi];
+}
+// c ? a : b on values (a conditional on two lvalues may become a select of their addresses, which
+// keeps the state arrays out of registers)
+template <typename T>
+__device__ __forceinline__ T pick(bool c, T a, T b) { return c ? a : b; }
+// two-min update with min1 <= min2 (values are selected, never rounded: any form is exact)
+__device__ __forceinline__ void two_min(float& m1, float& m2, float a) {
+    m2 = __builtin_amdgcn_fmed3f(m1, m2, a);
+    m1 = fminf(m1, a);
+}
+__device__ __forceinline__ void two_min(double& m1, double& m2, double a) {
+    m2 = fmin(m2, fmax(m1, a));
+    m1 = fmin(m1, a);
+}
+
+template <int BG, typename T, bool OFS>
+__device__ __forceinline__ void flood_body(
+    const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
+    int L, T alpha, T beta, int pc, const DecWork* __restrict__ work,
+    const CbRef* __restrict__ cbs) {
+    using P = BGT<BG>;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
+    constexpr int CS = kDecThreads;   // LDS column stride (entries) = slots per half
+    constexpr int NLS = kFloodPlan<BG, T>.nls;
+    constexpr int NS = kFloodPlan<BG, T>.nslot > 0 ? kFloodPlan<BG, T>.nslot : 1;
+    constexpr int NPW = kFloodPlan<BG, T>.npw > 0 ? kFloodPlan<BG, T>.npw : 1;
+    constexpr int ST_B = KC * CS * TS;               // LDS rows: (mA, mB) pairs
+    constexpr int PK_B = ST_B + NLS * CS * 2 * TS;   // LDS rows: sign/argmin words
+    constexpr int FLAG_B = PK_B + NLS * CS * 4;
+    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // wrap table, 2*CS entries
+    constexpr int KH = (KC + 1) / 2;   // own columns [0, KH) are half 0's, [KH, KC) half 1's
+    extern __shared__ __align__(16) unsigned char smem[];
+
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
+    int Zc = Zc_u, zi = zi_u, G = G_u;
+    const int t = threadIdx.x;
+    const int H = (int)(blockDim.x >> 1);   // slots per half, a multiple of 64
+    const int h = __builtin_amdgcn_readfirstlane(t >= H ? 1 : 0);
+    const int s = t - h * H;
+    if (work) {
+        DecWork w = work[blockIdx.x];
+        Zc = w.Zc, zi = w.zi, G = w.G;
+    }
+    // slot s = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
+    // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
+    const int z = s / G;
+    const int cbl = s - z * G;
+    bool valid = z < Zc;
+    const T* lrow = llr;
+    int8_t* crow = ck;
+    int out = 0;
+    if (valid) {
+        if (work) {
+            CbRef r = cbs[work[blockIdx.x].first + cbl];
+            lrow = llr + r.llr_off;
+            crow = ck + r.ck_off;
+            out = r.out;
+        } else {
+            const int cb = blockIdx.x * G + cbl;   // slots past the batch keep lrow = llr
+            valid = cb < B;
+            if (valid) {
+                lrow = llr + (int64_t)cb * ldl;
+                crow = ck + (int64_t)cb * ldc;
+                out = cb;
+            }
+        }
+    }
+    const int cl = valid ? cbl : 0;
+    const int so = valid ? s : 0;
+    const int tzb = so * TS;   // byte offset of this slot's own column entry
+    const int zg = valid ? z : 0;   // loads issued without a branch stay in row 0 of CB 0
+    int zv = zg, ziv = zi;
+    int* flagA = (int*)(smem + FLAG_B);
+    int* anyf = flagA + 2 * kMaxG;
+    int epoch = 0;
+    auto block_any = [&](bool p) -> bool {
+        ++epoch;
+        if (p) *anyf = epoch;
+        lds_barrier();
+        return *anyf == epoch;
+    };
+    using lds_T = __attribute__((address_space(3))) T;
+    using lds_V2 = __attribute__((address_space(3))) V2<T>;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
+    auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
+    auto llrx = [&](int i) -> T { return lrow[(KB + i - pc) * Zc + zv]; };   // ext column of row i
+
+    // row state: (mA, mB) magnitudes, the signs of r_k (edge 0 in bit d-1) and the argmin edge;
+    // VGPR rows of degree <= 12 keep signs | argmin << 12 in one 16-bit field of a shared word
+    T sA[NS], sB[NS];
+    uint32_t sP[NPW];
+#pragma unroll
+    for (int x = 0; x < NS; ++x) sA[x] = T(0), sB[x] = T(0);
+#pragma unroll
+    for (int x = 0; x < NPW; ++x) sP[x] = 0u;
+    // u: bit 31 = sign of r_0 (u << k: of r_k), idx: argmin edge
+    auto get_state = [&](auto ic, T& a, T& b, uint32_t& u, uint32_t& idx) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int d = BGT<BG>::RS[i + 1] - BGT<BG>::RS[i];
+        if constexpr (i < NLS) {
+            const V2<T> v = *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + (i * CS) * 2 * TS + 2 * tzb);
+            a = v.x, b = v.y;
+            const uint32_t p = *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + (i * CS) * 4 + so * 4);
+            u = p << (32 - d), idx = p >> 24;
+            asm volatile("" : "+v"(idx));   // compare idx itself with inline constants k
+        } else {
+            constexpr int x = kFloodPlan<BG, T>.slot[i];
+            constexpr int w = kFloodPlan<BG, T>.pw[i];
+            constexpr int f = kFloodPlan<BG, T>.ph[i];
+            a = sA[x], b = sB[x];
+            const uint32_t p = sP[w];
+            if constexpr (f == 0) u = p << (32 - d), idx = p >> 24;
+            else if constexpr (f == 1) u = p << (32 - d), idx = (p >> 12) & 0xfu;
+            else u = p << (16 - d), idx = p >> 28;
+            asm volatile("" : "+v"(idx));
+        }
+    };
+    auto put_state = [&](auto ic, T a, T b, uint32_t negs, uint32_t idx) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NLS) {
+            V2<T> v;
+            v.x = a, v.y = b;
+            *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + (i * CS) * 2 * TS + 2 * tzb) = v;
+            *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + (i * CS) * 4 + so * 4) = negs | (idx << 24);
+        } else {
+            constexpr int x = kFloodPlan<BG, T>.slot[i];
+            constexpr int w = kFloodPlan<BG, T>.pw[i];
+            constexpr int f = kFloodPlan<BG, T>.ph[i];
+            sA[x] = a, sB[x] = b;
+            if constexpr (f == 0) sP[w] = negs | (idx << 24);
+            else if constexpr (f == 1) sP[w] = (sP[w] & 0xffff0000u) | negs | (idx << 12);
+            else sP[w] = (sP[w] & 0xffffu) | (negs << 16) | (idx << 28);
+        }
+    };
+
+    // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS row state 0; wrap table
+    if (valid)
+        for (int j = h * KH; j < (h ? KC : KH); ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+    for (int w = t; w < NLS * CS; w += (int)blockDim.x) {
+        V2<T> v;
+        v.x = T(0), v.y = T(0);
+        *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + w * 2 * TS) = v;
+        *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + w * 4) = 0u;
+    }
+    if (s == 0 && h == 0)
+        for (int c = 0; c < G; ++c) flagA[c] = 0;
+    if (t == 0) *anyf = 0;
+    {
+        const int ZG = Zc * G;   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
+        for (int e = t; e < 2 * ZG; e += (int)blockDim.x)
+            *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + e * 4) = (uint32_t)((e < ZG ? e : e - ZG) * TS);
+    }
+    const uint32_t tzbT = (uint32_t)(TBL_B + so * 4);
+    const uint32_t G4 = (uint32_t)(G * 4);
+    bool active = valid;
+    lds_barrier();
+
+    // byte offset (without column base) of entry ((z + sft) mod Zc, cl): one wrap-table lookup
+    auto rot = [&](uint32_t base, int sft) -> int {
+        return (int)*(lds_u32*)(uintptr_t)(base + (uint32_t)sft * G4);
+    };
+    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
+    asm volatile("" : "+v"(mv));
+
+    int it = 0;
+    for (; it < L; ++it) {
+        // zv / ziv opaque per iteration: otherwise LICM hoists the ~300 loop-invariant shift
+        // words and column addresses out of the loop into registers
+        zv = zg;
+        ziv = zi;
+        asm volatile("" : "+v"(zv));
+        asm volatile("" : "+s"(ziv));
+        bool fail = false;
+        uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
+        // shift words of this lifting size: one base pointer (SGPR pair), immediate offsets
+        const uint32_t* __restrict__ swrow = shift_row<BG>(ziv);
+        auto sh = [&](int e) -> int {   // e compile-time after unrolling
+            const uint32_t w = swrow[e >> 1];
+            return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+        };
+
+        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202)
+        auto rowA = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            T mA, mB;
+            uint32_t u, idxo;   // u: bit 31 = sign of r_k for the edge k being visited
+            get_state(ic, mA, mB, u, idxo);
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const T rold = xsign_v(pick(idxo == (uint32_t)k, mB, mA), u, mv);
+                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
+                T a;
+                if constexpr (j < KC) {
+                    a = at(j * CS * TS + rot(tzbT, sh(e0 + k)));
+                } else {
+                    a = llrx(i) + rold;   // LQ of a degree-1 column = LLR + its only r
+                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                }
+                par ^= a < T(0);
+                const T q = a - rold;
+                const T aq = fabs(q);
+                idx = aq < min1 ? (uint32_t)k : idx;
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                two_min(min1, min2, aq);
+                sx ^= FT<T>::sbits(q);
+                // bound the LDS reads the scheduler hoists ahead (each holds 2 VGPRs in f64)
+                if constexpr (kSchedChunk > 0 && k % kSchedChunk == kSchedChunk - 1)
+                    __builtin_amdgcn_sched_barrier(0);
+            });
+            fail |= par;
+            T x1 = min1, x2 = min2;
+            if constexpr (OFS) {
+                x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
+                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const uint32_t flip = (uint32_t)((int32_t)sx >> 31) & ((1u << d) - 1u);
+            put_state(ic, alpha * x1, alpha * x2, negs ^ flip, idx);
+        };
+        if (active) {
+            sfor<0, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if (h == kFloodPlan<BG, T>.owner[i]) rowA(ic);
+            });
+            if (fail) flagA[cl] = 1;
+        }
+        lds_barrier();
+        // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
+        if (active && flagA[cl] == 0) {
+            for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
+            sfor<4, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if (h == kFloodPlan<BG, T>.owner[i]) crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
+            });
+            if (z == 0 && h == 0) status[out] = 1, iters[out] = it;
+            active = false;
+        }
+
+        // ---- phase B: Lr.sum(axis=0) in row order into the LQ array (:126)
+        auto rowB = [&](auto ic, auto splitc) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            constexpr int split = decltype(splitc)::value;   // -1: all edges, else edges of parity
+            T nA, nB;
+            uint32_t u, idxn;
+            get_state(ic, nA, nB, u, idxn);
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                constexpr int cidx = [] {
+                    int n = 0;
+                    for (int kk = 0; kk < k; ++kk) n += P::COL[e0 + kk] < KC;
+                    return n;
+                }();
+                if constexpr (j < KC && (split < 0 || (cidx & 1) == split)) {
+                    const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
+                    lds_T& acc = at(j * CS * TS + rot(tzbT, sh(e0 + k)));
+                    if constexpr (kFloodPlan<BG, T>.first_row[j] == i) acc = T(0) + r;
+                    else acc = acc + r;
+                }
+                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
+            });
+        };
+        sfor<0, kGroups<BG>.n>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if (active) {
+                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (i < NLS) {
+                        if (h == 0) rowB(ic, std::integral_constant<int, 0>{});
+                        else rowB(ic, std::integral_constant<int, 1>{});
+                    } else {
+                        if (h == kFloodPlan<BG, T>.owner[i]) rowB(ic, std::integral_constant<int, -1>{});
+                    }
+                });
+            }
+            lds_barrier();
+        });
+        // ---- LQ = LLRin + sum (:126) for the own entries
+        if (active)
+            for (int j = h * KH; j < (h ? KC : KH); ++j) {
+                lds_T& x = own(j);
+                x = (j < pc ? T(0) : lrow[(j - pc) * Zc + zv]) + x;
+            }
+        if (s == 0 && h == 0)
+            for (int c = 0; c < G; ++c) flagA[c] = 0;   // read before the phase-B barriers
+        if (!block_any(active)) break;
+    }
+
+    // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
+    zv = zg;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    auto rfinal = [&](auto ic, int k) -> T {
+        constexpr int i = decltype(ic)::value;
+        T a, b;
+        uint32_t u, idx;
+        get_state(ic, a, b, u, idx);
+        return xsign_v(pick(idx == (uint32_t)k, b, a), u << k, mv);
+    };
+    if (active) {
+        bool fail = false;
+        sfor<0, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            if (h == kFloodPlan<BG, T>.owner[i]) {
+                bool par = false;
+                sfor<0, d>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int j = P::COL[e0 + k];
+                    T a;
+                    if constexpr (j < KC) a = at(j * CS * TS + rot(tzbT, shift_of<BG>(zi, e0 + k)));
+                    else a = llrx(i) + rfinal(ic, k);
+                    par ^= (a <= T(0));
+                });
+                fail |= par;
+            }
+        });
+        if (fail) flagA[cl] = 1;
+    }
+    lds_barrier();
+    if (active) {
+        for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+        sfor<4, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+            if (h == kFloodPlan<BG, T>.owner[i]) crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
+        });
+        if (z == 0 && h == 0) {
+            status[out] = flagA[cl] == 0;
+            iters[out] = L;
+        }
+    }
+}
+
+template <int BG, typename T, bool OFS>
+__global__ __launch_bounds__(kFloodThreads) __attribute__((amdgpu_waves_per_eu(3))) void
+ldpc_flood_kernel(LDPC5G_DEC_PARAMS) {
+    flood_body<BG, T, OFS>(LDPC5G_DEC_ARGS);
+}
+
+template <int BG, typename T, bool OFS>
+constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS>; }
+
+template <int BG, typename T>
+size_t flood_lds_bytes() {
+    static_assert(flood_lds_bytes_t<BG, T>() <= kLdsPerCU, "LDS budget of one CU");
+    return flood_lds_bytes_t<BG, T>();
+}
+
+template <int BG, typename T>
+int set_flood_lds(bool ofs) {
+    const size_t lds = flood_lds_bytes<BG, T>();
+    return ofs ? set_lds_once<flood_kernel<BG, T, true>()>(lds)
+               : set_lds_once<flood_kernel<BG, T, false>()>(lds);
+}
+
+template <int BG, typename T>
+int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                   int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true> : ldpc_flood_kernel<BG, T, false>;
+    // small batches (the per-codeblock drop-ins): no more slots than codeblocks
+    const int G = std::min(dec_G(Zc, false), B);
+    const int H = ((G * Zc + 63) / 64) * 64;
+    const int grid = (B + G - 1) / G;
+    if (int rc = set_flood_lds<BG, T>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T>();
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(2 * H), lds, st, llr, ck, status,
+                       iters, B, Zc, zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc,
+                       (const DecWork*)nullptr, (const CbRef*)nullptr);
+    return check_hip(hipGetLastError(), "ldpc_flood_kernel launch");
+}
+
+template <int BG, typename T>
+int launch_flood_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                         const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
+                         int pc, hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true> : ldpc_flood_kernel<BG, T, false>;
+    if (int rc = set_flood_lds<BG, T>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T>();
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodThreads), lds, st, llr, ck,
+                       status, iters, 0, 0, 0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc,
+                       work, cbs);
+    return check_hip(hipGetLastError(), "ldpc_flood_kernel(mixed) launch");
+}
+
+template <int BG, typename T>
+int flood_blocks_per_cu_t() {
+    const size_t lds = flood_lds_bytes<BG, T>();
+    if (set_lds_once<flood_kernel<BG, T, false>()>(lds)) return -1;
+    int n = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ldpc_flood_kernel<BG, T, false>, kFloodThreads, lds) !=
+        hipSuccess)
+        return -1;
+    return n;
+}
+
+}  // namespace
+}  // namespace ldpc5g_impl
