@@ -32,7 +32,7 @@ HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip 
 # committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false>",
-              "flooding": "void ldpc_dec_kernel<1, float, false>"}
+              "flooding": "void ldpc_flood_kernel<1, float, false>"}
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
 
@@ -444,7 +444,7 @@ def main():
                          "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
                          "frac": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12
                                        / VALU_PEAK_TLANE, 4),
-                         "kernel": "void ldpc_dec_kernel<1, double, false>",
+                         "kernel": "void ldpc_flood_kernel<1, double, false>",
                          "hbm_achieved_GBps": round(B * DEC64_BYTES_PER_CB / f64_launch / 1e9, 2),
                          "algorithmic_bytes_per_cb": DEC64_BYTES_PER_CB,
                          "note": "same 13 lane-ops per edge-update in float64 against the "

@@ -1,8 +1,7 @@
-// ldpc5g_dec_body.h — flooding / layered min-sum decoder kernels (py5gphy/ldpc/nr_ldpc_decode.py:
-// 11-143, 178-227), included by ldpc5g_dec.hip (flooding instantiations) and ldpc5g_dec_l.hip
-// (layered instantiations).  The two translation units are compiled with different vectorizer
-// settings (build.py NO_SLP): SLP-formed v_pk_add_f32 helps the flooding kernel and hurts the
-// layered one.  Reference mapping in ldpc5g_common.h / DESIGN.md §4.
+// ldpc5g_dec_body.h — layered min-sum decoder kernel (the perf schedule of py5gphy/ldpc/
+// nr_ldpc_decode.py:51-143's min-sum) and the helpers the flooding decoder
+// (ldpc5g_dec_flood.h) shares.  Instantiated by ldpc5g_dec_l.hip, which is built without the SLP
+// vectorizer (build.py NO_SLP).  Reference mapping in ldpc5g_common.h / DESIGN.md §4.
 #pragma once
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,16 +42,9 @@ struct FT<double> {
 template <typename T>
 using V2 = T __attribute__((ext_vector_type(2)));
 
-// Compressed check-node state of one row: r_k = (k == idx ? mB : mA), sign = bit k of pk.
-// pk: bits 0..deg-1 = sign of r_k, bits 24..28 = idx (an edge holding min |q|).
-template <typename T>
-__device__ __forceinline__ T decomp(T mA, T mB, uint32_t pk, uint32_t idx, int k) {
-    return FT<T>::xsign((idx == (uint32_t)k) ? mB : mA, pk << (31 - k));
-}
-
 // Layered state: mA/mB carry the row sign (product of all q signs), pk bits d-1-k hold the sign
 // of q_k (packed with v_alignbit, edge 0 highest), bits 24..28 the argmin edge.  Then
-// r_k = (k == idx ? mB : mA) with its sign flipped by sign(q_k) — the same value as decomp().
+// r_k = (k == idx ? mB : mA) with its sign flipped by sign(q_k).
 template <typename T>
 __device__ __forceinline__ T decomp_l(T mAs, T mBs, uint32_t pk, uint32_t idx, int d, int k) {
     return FT<T>::xsign((idx == (uint32_t)k) ? mBs : mAs, pk << (32 - d + k));
@@ -108,12 +100,6 @@ __device__ __forceinline__ uint32_t shift_word(int zi, int w) {
 }
 
 
-// Ext (degree-1) column LLRs are staged in LDS only by the float32 flooding kernel; the layered
-// kernel reads them from global memory one row group ahead, which keeps its LDS at ~40 KB so two
-// workgroups (12 waves, 3 per SIMD) share a CU.
-template <typename T, bool LAYERED>
-constexpr bool xl_lds() { return sizeof(T) == 4 && !LAYERED; }
-
 // Layered: the (mA, mB) magnitudes of the first kLdsRows rows live in LDS rather than VGPRs, so
 // the kernel fits the 168-VGPR budget of 3 waves/SIMD without scratch spills (spilling kernels
 // are held to fewer resident waves).  2 x (40 KB APP + 33 KB state + 3 KB flags) <= 160 KB.
@@ -123,18 +109,17 @@ constexpr int lds_rows() { return BG == 1 ? 11 : 18; }
 // (Variants measured and dropped are listed in DESIGN.md §4.2; tools/ab/make_variants.py rebuilds
 // them as separate libraries for side-by-side timing.)
 constexpr int kRecompDeg = 12;
-// LDS column stride (entries) = workgroup size: 384 for flooding, 768 for layered
+// LDS column stride (entries) = workgroup size: 768 for layered (the flooding kernel: 384 slots)
 template <bool LAYERED>
 constexpr int dec_cs() { return LAYERED ? kDecThreadsL : kDecThreads; }
 constexpr int kMaxG = kDecThreadsL / 2;   // = 768 / min Zc (2): per-CB-slot flag entries
 
+// APP of the core columns, (mA, mB) of the first lds_rows rows, flags, wrap table
 template <int BG, typename T, bool LAYERED>
 constexpr size_t dec_lds_bytes_t() {
     constexpr size_t CS = dec_cs<LAYERED>();
-    return (size_t)BGT<BG>::KC * CS * sizeof(T) * (LAYERED ? 1 : 2) +
-           (xl_lds<T, LAYERED>() ? (size_t)(BGT<BG>::MB - 4) * CS * sizeof(T) : 0) +
-           (LAYERED ? (size_t)2 * lds_rows<BG>() * CS * sizeof(T) : 0) + (2 * kMaxG + 4) * sizeof(int) +
-           (LAYERED ? (size_t)2 * CS * sizeof(uint32_t) : 0);
+    return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)2 * lds_rows<BG>() * CS * sizeof(T) +
+           (2 * kMaxG + 4) * sizeof(int) + (size_t)2 * CS * sizeof(uint32_t);
 }
 
 // Layered state words: rows 0..3 one word each (negs | idx << 24); rows >= 4 (degree <= 12) two
@@ -175,17 +160,15 @@ __device__ __forceinline__ void dec_body(
     const CbRef* __restrict__ cbs) {
     // pc = number of leading punctured block columns absent from the LLR rows (2, or 0 when the
     // caller passes full-length rows as decode_ldpc(LLRin, H, ...) does, nr_ldpc_decode.py:51)
+    static_assert(LAYERED, "the flooding schedule is ldpc5g_dec_flood.h");
     using P = BGT<BG>;
     constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
     constexpr int CS = dec_cs<LAYERED>();   // LDS column stride = workgroup size
-    constexpr bool XL_LDS = xl_lds<T, LAYERED>();
-    static_assert(!LAYERED || ext_rows_fit16<BG>(), "packed layered state needs degree <= 12");
-    constexpr int ACC_B = KC * CS * TS;                        // byte offsets in LDS
-    constexpr int XL_B = KC * CS * TS * (LAYERED ? 1 : 2);
-    constexpr int ST_B = XL_B + (XL_LDS ? (MB - 4) * CS * TS : 0);   // layered: LDS row state
-    constexpr int NLR = LAYERED ? lds_rows<BG>() : 0;
+    static_assert(ext_rows_fit16<BG>(), "packed layered state needs degree <= 12");
+    constexpr int ST_B = KC * CS * TS;   // byte offsets in LDS: APP, then the LDS row state
+    constexpr int NLR = lds_rows<BG>();
     constexpr int FLAG_B = ST_B + 2 * NLR * CS * TS;
-    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // layered: wrap table, 2*CS entries
+    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // wrap table, 2*CS entries
     extern __shared__ __align__(16) unsigned char smem[];
 
     if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
@@ -250,13 +233,10 @@ __device__ __forceinline__ void dec_body(
     auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
     auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
     // channel LLR of the degree-1 extension column of row i = 4 + i4 (own column z)
-    auto llrx = [&](int i4) -> T {
-        if constexpr (XL_LDS) return at(XL_B + i4 * CS * TS + tzb);
-        else return lrow[(KB + 4 + i4 - pc) * Zc + zv];
-    };
+    auto llrx = [&](int i4) -> T { return lrow[(KB + 4 + i4 - pc) * Zc + zv]; };
 
     // per-thread state of rows (i, z), i = 0..MB-1
-    constexpr int NSP = LAYERED ? 4 + (MB - 3) / 2 : MB;
+    constexpr int NSP = 4 + (MB - 3) / 2;
     T sA[MB], sB[MB];
     uint32_t sP[NSP];
 #pragma unroll
@@ -288,7 +268,7 @@ __device__ __forceinline__ void dec_body(
     auto get_row = [&](auto ic) -> uint32_t {
         constexpr int i = decltype(ic)::value;
         constexpr int d = P::RS[i + 1] - P::RS[i];
-        if constexpr (!LAYERED || i < 4) {
+        if constexpr (i < 4) {
             return sP[i];
         } else {
             constexpr int w = 4 + (i - 4) / 2;
@@ -298,7 +278,7 @@ __device__ __forceinline__ void dec_body(
     };
     auto put_row = [&](auto ic, uint32_t negs, uint32_t idx) {
         constexpr int i = decltype(ic)::value;
-        if constexpr (!LAYERED || i < 4) {
+        if constexpr (i < 4) {
             sP[i] = negs | (idx << 24);
         } else {
             constexpr int w = 4 + (i - 4) / 2;
@@ -307,26 +287,22 @@ __device__ __forceinline__ void dec_body(
         }
     };
 
-    uint32_t hdc_prev = 0;   // layered: hard decisions of own core columns, last iteration end
-    uint64_t hdx_prev = 0;   // layered: ... of own extension columns
+    uint32_t hdc_prev = 0;   // hard decisions of own core columns, last iteration end
+    uint64_t hdx_prev = 0;   // ... of own extension columns
     if (valid) {
         for (int j = 0; j < KC; ++j) {
             const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
             own(j) = v;
-            if (!LAYERED) at(ACC_B + j * CS * TS + tzb) = T(0);
             hdc_prev |= (uint32_t)(v < T(0)) << j;
         }
-        for (int i4 = 0; i4 < MB - 4; ++i4) {
-            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
-            if constexpr (XL_LDS) at(XL_B + i4 * CS * TS + tzb) = v;
-            hdx_prev |= (uint64_t)(v < T(0)) << i4;
-        }
+        for (int i4 = 0; i4 < MB - 4; ++i4)
+            hdx_prev |= (uint64_t)(lrow[(KB + 4 + i4 - pc) * Zc + z] < T(0)) << i4;
     }
     for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);
     if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
     if (t == 0) *anyf = 0;
     using lds_u32 = __attribute__((address_space(3))) uint32_t;
-    if constexpr (LAYERED) {   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
+    {   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
         const int ZG = Zc * G;
         if (t < ZG) {
             *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + t * 4) = (uint32_t)(t * 4);
@@ -356,76 +332,7 @@ __device__ __forceinline__ void dec_body(
         asm volatile("" : "+v"(zv));
         asm volatile("" : "+s"(ziv));
         bool fail = false;
-        uint64_t hdx = 0;   // flooding: ext hard decisions at pass start; layered: at pass end
-        // ---- flooding row i (reference order, nr_ldpc_decode.py:117-131)
-        auto flooding_row = [&](auto ic, auto& gshift) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i];
-            constexpr int d = P::RS[i + 1] - e0;
-            const T mA = sA[i], mB = sB[i];
-            const uint32_t pk = sP[i];
-            const uint32_t idxo = pk >> 24;
-            T q[d];
-            int rb[d];
-            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-            uint32_t sx = 0, idx = 0, negs = 0;
-            bool par = false;
-            // pass 1: variable-to-check messages q = LQ - Lr, two-min, sign product
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int j = P::COL[e0 + k];
-                const T rold = decomp(mA, mB, pk, idxo, k);
-                T a;
-                if constexpr (j < KC) {
-                    rb[k] = rot(gshift(e0 + k));
-                    a = at(j * CS * TS + rb[k]);
-                } else {
-                    a = llrx(i - 4) + rold;   // LQ of a degree-1 column
-                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
-                }
-                par ^= a < T(0);
-                const T qq = a - rold;
-                q[k] = qq;
-                const T aq = fabs(qq);
-                idx = aq < min1 ? (uint32_t)k : idx;
-                negs |= (FT<T>::sbits(qq) >> 31) << k;
-                min2 = FT<T>::med3(min1, min2, aq);
-                min1 = fmin(min1, aq);
-                sx ^= FT<T>::sbits(qq);
-            });
-            fail |= par;
-            const T x1 = min1 - beta, x2 = min2 - beta;
-            const T nA = alpha * (x1 > T(0) ? x1 : T(0));   // (:201-202)
-            const T nB = alpha * (x2 > T(0) ? x2 : T(0));
-            // pass 2: Lr = sign * (k == argmin ? nB : nA), accumulated row-ascending (:126).
-            // High-degree rows recompute their rotated addresses (see layered_row).
-            constexpr bool RECOMP = d > kRecompDeg;
-            uint32_t tzb2 = (uint32_t)tzb, tzbw2 = tzbw;
-            if constexpr (RECOMP) {
-                asm volatile("" : "+v"(tzb2));
-                asm volatile("" : "+v"(tzbw2));
-            }
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int j = P::COL[e0 + k];
-                if constexpr (j < KC) {
-                    const uint32_t sb = (negs >> k ^ sx >> 31) << 31;
-                    const T r = FT<T>::xsign(idx == (uint32_t)k ? nB : nA, sb);
-                    int rbk;
-                    if constexpr (RECOMP) {
-                        const uint32_t S = (uint32_t)gshift(e0 + k) * GT;
-                        rbk = (int)min(tzb2 + S, tzbw2 + S);
-                    } else {
-                        rbk = rb[k];
-                    }
-                    lds_T& acc = at(ACC_B + j * CS * TS + rbk);
-                    acc = acc + r;
-                }
-            });
-            sA[i] = nA;
-            sB[i] = nB;
-            sP[i] = (negs ^ ((sx >> 31) ? ((1u << d) - 1u) : 0u)) | (idx << 24);
-        };
+        uint64_t hdx = 0;   // ext hard decisions at the end of the pass
         // ---- layered row i: q = APP - r_old, APP = q + r_new.
         //      Op choice follows the gfx950 VALU rates measured by tools/microbench/valu_rates.hip: f32
         //      add/sub and all-VGPR bitwise ops (and, xor, bitop3, u32 add) issue at twice the
@@ -520,13 +427,11 @@ __device__ __forceinline__ void dec_body(
         // group g - 1, so a whole group's work hides the L2 / Infinity-Cache latency
         auto prefetch_xl = [&](auto gc) {
             constexpr int g = decltype(gc)::value;
-            if constexpr (LAYERED) {
-                constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
-                sfor<r0, (kGroups<BG>.start[g + 1] > r0 ? kGroups<BG>.start[g + 1] : r0)>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];   // unconditional: see zg
-                });
-            }
+            constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
+            sfor<r0, (kGroups<BG>.start[g + 1] > r0 ? kGroups<BG>.start[g + 1] : r0)>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];   // unconditional: see zg
+            });
         };
         prefetch(std::integral_constant<int, 0>{});
         prefetch_xl(std::integral_constant<int, 0>{});   // row 0 has no ext column: no load
@@ -544,34 +449,14 @@ __device__ __forceinline__ void dec_body(
                 sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
                     constexpr int i = decltype(ic)::value;
                     constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
-                    if constexpr (LAYERED) layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));
-                    else flooding_row(ic, gshift);
+                    layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));
                 });
             }
             if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
             lds_barrier();
         });
 
-        if constexpr (!LAYERED) {
-            // ---- reference order: the syndrome of LQ at the start of the pass decides (:107-114)
-            if (active && fail) flagA[cl] = 1;
-            lds_barrier();
-            const bool conv = active && flagA[cl] == 0;
-            if (conv) {
-                for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
-                for (int i4 = 0; i4 < MB - 4; ++i4)
-                    crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
-                if (z == 0) status[out] = 1, iters[out] = it;
-                active = false;
-            } else if (active) {
-                for (int j = 0; j < KC; ++j) {
-                    lds_T& acc = at(ACC_B + j * CS * TS + tzb);
-                    const T lf = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
-                    own(j) = lf + acc;   // LQ = LLR + sum Lr (:126)
-                    acc = T(0);
-                }
-            }
-        } else {
+        {
             // ---- layered stopping rule: no hard decision changed over the iteration, then an
             //      exact syndrome check of those decisions (oracle.decode_layered)
             uint32_t hdc = 0;
@@ -619,13 +504,8 @@ __device__ __forceinline__ void dec_body(
 
     // r of edge k of row i from the stored state (layout depends on the schedule)
     auto rfinal = [&](auto ic, int d, int k) -> T {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (LAYERED) {
-            const uint32_t pk = get_row(ic);
-            return decomp_l(getA(ic), getB(ic), pk, pk >> 24, d, k);
-        } else {
-            return decomp(sA[i], sB[i], sP[i], sP[i] >> 24, k);
-        }
+        const uint32_t pk = get_row(ic);
+        return decomp_l(getA(ic), getB(ic), pk, pk >> 24, d, k);
     };
     // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
     zv = z;
@@ -673,11 +553,6 @@ __device__ __forceinline__ void dec_body(
 #define LDPC5G_DEC_ARGS \
     llr, ck, status, iters, B, Zc_u, zi_u, G_u, ldl, ldc, L, alpha, beta, pc, work, cbs
 
-// flooding (float64 / float32): one workgroup per CU (VGPR-bound)
-template <int BG, typename T, bool LAYERED>
-__global__ __launch_bounds__(kDecThreads) void ldpc_dec_kernel(LDPC5G_DEC_PARAMS) {
-    dec_body<BG, T, LAYERED>(LDPC5G_DEC_ARGS);
-}
 // layered float32: 768 threads = 12 waves = 3 per SIMD (<= 168 VGPRs), G = floor(768/Zc) CBs
 template <int BG, typename T, bool LAYERED, bool OFS>
 __global__ __launch_bounds__(kDecThreadsL) __attribute__((amdgpu_waves_per_eu(3))) void
@@ -686,8 +561,8 @@ ldpc_dec_kernel_l(LDPC5G_DEC_PARAMS) {
 }
 template <int BG, typename T, bool LAYERED, bool OFS = true>
 constexpr auto dec_kernel() {
-    if constexpr (LAYERED) return ldpc_dec_kernel_l<BG, T, LAYERED, OFS>;
-    else return ldpc_dec_kernel<BG, T, LAYERED>;
+    static_assert(LAYERED, "the flooding kernels are in ldpc5g_dec_flood.h");
+    return ldpc_dec_kernel_l<BG, T, LAYERED, OFS>;
 }
 
 template <int BG, typename T, bool LAYERED>

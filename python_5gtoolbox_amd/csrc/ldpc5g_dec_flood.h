@@ -26,10 +26,11 @@ namespace {
 
 constexpr int kFloodThreads = 2 * kDecThreads;   // two halves of 384 slots
 constexpr size_t kLdsPerCU = 160 * 1024;
-#ifndef LDPC5G_FLOOD_CHUNK
-#define LDPC5G_FLOOD_CHUNK 6
+#ifndef LDPC5G_FLOOD_XPRE
+#define LDPC5G_FLOOD_XPRE 4
 #endif
-constexpr int kSchedChunk = LDPC5G_FLOOD_CHUNK;
+// extension-column LLRs are loaded this many ext rows ahead of their use in phase A
+constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 
 template <int BG, typename T>
 struct FloodPlan {
@@ -41,12 +42,15 @@ struct FloodPlan {
     int ph[64] = {};      // 0: whole word (negs | idx << 24), 1: low field, 2: high field (negs | idx << 12)
     int npw = 0;
     int first_row[32] = {};   // lowest base row of core column j (writes 0 + r in phase B)
+    int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner half's ext rows
+    int xlist[2][64] = {};    // ext rows of each half, ascending
+    int nx[2] = {0, 0};
     static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
     constexpr FloodPlan() {
         using P = BGT<BG>;
         constexpr int CS = kDecThreads;
         const auto& G = kGroups<BG>;
-        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4 + 2 * CS * 4;
+        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4;
         const int fit = (int)((kLdsPerCU - fixed) / (CS * (2 * sizeof(T) + 4)));
         int lead = 0;   // leading single-row groups: their phase B is split only if in LDS
         while (lead < G.n && G.start[lead + 1] - G.start[lead] == 1 && G.start[lead] == lead) ++lead;
@@ -90,6 +94,10 @@ struct FloodPlan {
             }
             npw = npw > n ? npw : n;
         }
+        for (int i = 4; i < P::MB; ++i) {
+            xpos[i] = nx[owner[i]];
+            xlist[owner[i]][nx[owner[i]]++] = i;
+        }
         for (int j = 0; j < P::KC; ++j) {
             first_row[j] = -1;
             for (int i = 0; i < P::MB && first_row[j] < 0; ++i)
@@ -105,7 +113,7 @@ template <int BG, typename T>
 constexpr size_t flood_lds_bytes_t() {
     constexpr int CS = kDecThreads;
     return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T>.nls * CS * (2 * sizeof(T) + 4) +
-           (2 * kMaxG + 4) * 4 + 2 * CS * 4;
+           (2 * kMaxG + 4) * 4;
 }
 
 // x with its sign flipped by bit 31 of u (all-VGPR v_bitop3: x ^ (u & mv), mv = 0x80000000)
@@ -150,7 +158,6 @@ __device__ __forceinline__ void flood_body(
     constexpr int ST_B = KC * CS * TS;               // LDS rows: (mA, mB) pairs
     constexpr int PK_B = ST_B + NLS * CS * 2 * TS;   // LDS rows: sign/argmin words
     constexpr int FLAG_B = PK_B + NLS * CS * 4;
-    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // wrap table, 2*CS entries
     constexpr int KH = (KC + 1) / 2;   // own columns [0, KH) are half 0's, [KH, KC) half 1's
     extern __shared__ __align__(16) unsigned char smem[];
 
@@ -270,19 +277,23 @@ __device__ __forceinline__ void flood_body(
     if (s == 0 && h == 0)
         for (int c = 0; c < G; ++c) flagA[c] = 0;
     if (t == 0) *anyf = 0;
-    {
-        const int ZG = Zc * G;   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
-        for (int e = t; e < 2 * ZG; e += (int)blockDim.x)
-            *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + e * 4) = (uint32_t)((e < ZG ? e : e - ZG) * TS);
-    }
-    const uint32_t tzbT = (uint32_t)(TBL_B + so * 4);
-    const uint32_t G4 = (uint32_t)(G * 4);
     bool active = valid;
     lds_barrier();
 
-    // byte offset (without column base) of entry ((z + sft) mod Zc, cl): one wrap-table lookup
-    auto rot = [&](uint32_t base, int sft) -> int {
-        return (int)*(lds_u32*)(uintptr_t)(base + (uint32_t)sft * G4);
+    // byte offset (without column base) of entry ((z + sft) mod Zc, cl): the unwrapped candidate,
+    // or the wrapped one when it is valid (smaller as unsigned).  Arithmetic, not the layered
+    // kernel's LDS wrap table: phase B is a chain of dependent LDS round trips per row group, and
+    // a table lookup adds one (measured: 4.85 -> 4.53 ms per 4096 f64 codeblocks without it)
+    const uint32_t GT = (uint32_t)(G * TS), tzbw = (uint32_t)tzb - (uint32_t)(Zc * G * TS);
+    auto rot = [&](int sft) -> int {
+        const uint32_t S = (uint32_t)sft * GT;
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
+    // f(integral_constant<half>): each half's rows form one basic block, so the scheduler can
+    // overlap a row's LDS reads with the previous row's arithmetic
+    auto per_half = [&](auto&& f) {
+        if (h == 0) f(std::integral_constant<int, 0>{});
+        else f(std::integral_constant<int, 1>{});
     };
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
     asm volatile("" : "+v"(mv));
@@ -304,6 +315,14 @@ __device__ __forceinline__ void flood_body(
             return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
         };
 
+        // ext LLR ring: slot p % XP holds the LLR of the half's ext row p, loaded XP rows ahead
+        constexpr int XP = kXPre > 0 ? kXPre : 1;
+        T xr[XP];
+        auto xload = [&](auto hc, auto pc_) {
+            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
+            if constexpr (kXPre > 0 && p < kFloodPlan<BG, T>.nx[hh])
+                xr[p % XP] = llrx(kFloodPlan<BG, T>.xlist[hh][p]);
+        };
         // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202)
         auto rowA = [&](auto ic) {
             constexpr int i = decltype(ic)::value;
@@ -322,21 +341,26 @@ __device__ __forceinline__ void flood_body(
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
                 T a;
                 if constexpr (j < KC) {
-                    a = at(j * CS * TS + rot(tzbT, sh(e0 + k)));
+                    a = at(j * CS * TS + rot(sh(e0 + k)));
                 } else {
-                    a = llrx(i) + rold;   // LQ of a degree-1 column = LLR + its only r
+                    constexpr int hh = kFloodPlan<BG, T>.owner[i], p = kFloodPlan<BG, T>.xpos[i];
+                    if constexpr (kXPre > 0) {
+                        a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
+                        xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+                    } else {
+                        a = llrx(i) + rold;
+                    }
                     hdx |= (uint64_t)(a < T(0)) << (i - 4);
                 }
                 par ^= a < T(0);
                 const T q = a - rold;
                 const T aq = fabs(q);
                 idx = aq < min1 ? (uint32_t)k : idx;
+                asm volatile("" : "+v"(idx));   // update in place: a sunk select chain keeps all
+                                                // the compare masks live (scratch spills)
                 negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
                 two_min(min1, min2, aq);
                 sx ^= FT<T>::sbits(q);
-                // bound the LDS reads the scheduler hoists ahead (each holds 2 VGPRs in f64)
-                if constexpr (kSchedChunk > 0 && k % kSchedChunk == kSchedChunk - 1)
-                    __builtin_amdgcn_sched_barrier(0);
             });
             fail |= par;
             T x1 = min1, x2 = min2;
@@ -348,33 +372,55 @@ __device__ __forceinline__ void flood_body(
             put_state(ic, alpha * x1, alpha * x2, negs ^ flip, idx);
         };
         if (active) {
-            sfor<0, MB>([&](auto ic) {
+            per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
+            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
                 constexpr int i = decltype(ic)::value;
                 if (h == kFloodPlan<BG, T>.owner[i]) rowA(ic);
             });
             if (fail) flagA[cl] = 1;
         }
+        // phase B's shift words are loaded one row group ahead (scalar loads issued before the
+        // barrier that precedes the group, so their latency hides behind it)
+        constexpr int NPW = max_group_nw<BG>();
+        uint32_t nsw[NPW];
+        auto prefetch = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            sfor<0, group_nw<BG>(g)>([&](auto wc) {
+                constexpr int w = decltype(wc)::value;
+                nsw[w] = swrow[group_w0<BG>(g) + w];
+            });
+        };
+        // the LDS-held state of the next group's row (rows < NLS are single-row groups) is read
+        // one group ahead as well: phase A wrote it before the barrier that precedes phase B
+        T qA = T(0), qB = T(0);
+        uint32_t qu = 0, qidx = 0;
+        auto prefetch_state = [&](auto gc) {
+            constexpr int r = kGroups<BG>.start[decltype(gc)::value];
+            if constexpr (r < NLS) get_state(std::integral_constant<int, r>{}, qA, qB, qu, qidx);
+        };
+        prefetch(std::integral_constant<int, 0>{});
         lds_barrier();
+        prefetch_state(std::integral_constant<int, 0>{});
         // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
         if (active && flagA[cl] == 0) {
             for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
-            sfor<4, MB>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                if (h == kFloodPlan<BG, T>.owner[i]) crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
+            per_half([&](auto hc) {
+                sfor<4, MB>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value)
+                        crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
+                });
             });
             if (z == 0 && h == 0) status[out] = 1, iters[out] = it;
             active = false;
         }
 
         // ---- phase B: Lr.sum(axis=0) in row order into the LQ array (:126)
-        auto rowB = [&](auto ic, auto splitc) {
+        auto rowB = [&](auto ic, auto splitc, auto& gshift, T nA, T nB, uint32_t u, uint32_t idxn) {
             constexpr int i = decltype(ic)::value;
             constexpr int e0 = P::RS[i];
             constexpr int d = P::RS[i + 1] - e0;
             constexpr int split = decltype(splitc)::value;   // -1: all edges, else edges of parity
-            T nA, nB;
-            uint32_t u, idxn;
-            get_state(ic, nA, nB, u, idxn);
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
@@ -385,34 +431,63 @@ __device__ __forceinline__ void flood_body(
                 }();
                 if constexpr (j < KC && (split < 0 || (cidx & 1) == split)) {
                     const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
-                    lds_T& acc = at(j * CS * TS + rot(tzbT, sh(e0 + k)));
+                    lds_T& acc = at(j * CS * TS + rot(gshift(e0 + k)));
                     if constexpr (kFloodPlan<BG, T>.first_row[j] == i) acc = T(0) + r;
                     else acc = acc + r;
                 }
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
             });
         };
+        // the core LLRs of the LQ update, loaded now so phase B hides their latency
+        T lf[KH];
+        if (active)
+            sfor<0, KH>([&](auto jc) {
+                constexpr int jj = decltype(jc)::value;
+                const int j = h * KH + jj;
+                if (j < KC) lf[jj] = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
+            });
         sfor<0, kGroups<BG>.n>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
+            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
+            const T cA = qA, cB = qB;
+            const uint32_t cu = qu, cidx = qidx;
+            if constexpr (g + 1 < kGroups<BG>.n) {
+                prefetch(std::integral_constant<int, g + 1>{});
+                prefetch_state(std::integral_constant<int, g + 1>{});
+            }
+            auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
+                return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+            };
             if (active) {
-                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    if constexpr (i < NLS) {
-                        if (h == 0) rowB(ic, std::integral_constant<int, 0>{});
-                        else rowB(ic, std::integral_constant<int, 1>{});
-                    } else {
-                        if (h == kFloodPlan<BG, T>.owner[i]) rowB(ic, std::integral_constant<int, -1>{});
-                    }
+                per_half([&](auto hc) {
+                    sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        if constexpr (i < NLS) {   // LDS state: both halves, alternate edges
+                            rowB(ic, hc, gshift, cA, cB, cu, cidx);
+                        } else if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {
+                            T a, b;
+                            uint32_t u, x;
+                            get_state(ic, a, b, u, x);
+                            rowB(ic, std::integral_constant<int, -1>{}, gshift, a, b, u, x);
+                        }
+                    });
                 });
             }
             lds_barrier();
         });
         // ---- LQ = LLRin + sum (:126) for the own entries
         if (active)
-            for (int j = h * KH; j < (h ? KC : KH); ++j) {
-                lds_T& x = own(j);
-                x = (j < pc ? T(0) : lrow[(j - pc) * Zc + zv]) + x;
-            }
+            sfor<0, KH>([&](auto jc) {
+                constexpr int jj = decltype(jc)::value;
+                const int j = h * KH + jj;
+                if (j < KC) {
+                    lds_T& x = own(j);
+                    x = lf[jj] + x;
+                }
+            });
         if (s == 0 && h == 0)
             for (int c = 0; c < G; ++c) flagA[c] = 0;   // read before the phase-B barriers
         if (!block_any(active)) break;
@@ -430,32 +505,37 @@ __device__ __forceinline__ void flood_body(
     };
     if (active) {
         bool fail = false;
-        sfor<0, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i];
-            constexpr int d = P::RS[i + 1] - e0;
-            if (h == kFloodPlan<BG, T>.owner[i]) {
-                bool par = false;
-                sfor<0, d>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int j = P::COL[e0 + k];
-                    T a;
-                    if constexpr (j < KC) a = at(j * CS * TS + rot(tzbT, shift_of<BG>(zi, e0 + k)));
-                    else a = llrx(i) + rfinal(ic, k);
-                    par ^= (a <= T(0));
-                });
-                fail |= par;
-            }
+        per_half([&](auto hc) {
+            sfor<0, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                constexpr int e0 = P::RS[i];
+                constexpr int d = P::RS[i + 1] - e0;
+                if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {
+                    bool par = false;
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        T a;
+                        if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                        else a = llrx(i) + rfinal(ic, k);
+                        par ^= (a <= T(0));
+                    });
+                    fail |= par;
+                }
+            });
         });
         if (fail) flagA[cl] = 1;
     }
     lds_barrier();
     if (active) {
         for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
-        sfor<4, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
-            if (h == kFloodPlan<BG, T>.owner[i]) crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
+        per_half([&](auto hc) {
+            sfor<4, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+                if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value)
+                    crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
+            });
         });
         if (z == 0 && h == 0) {
             status[out] = flagA[cl] == 0;

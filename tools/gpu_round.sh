@@ -76,8 +76,9 @@ if has pmc; then
              "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
              "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
     i=$((i + 1))
+    # PMC_ARGS: the profiled program's arguments (default: the headline bench)
     timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc$i" -o run -- \
-        python -u "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-extras \
+        python -u ${PMC_ARGS:-"$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-extras} \
         > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || { tail -5 "$OUT/pmc$i.err"; cd "$ROOT"; die "pmc $ctr" $?; }
   done
   cd "$ROOT"

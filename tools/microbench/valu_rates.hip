@@ -5,8 +5,8 @@
 #include <stdint.h>
 #define N_ITER 32768
 template <int OP> __global__ void kern(float* out, uint32_t sv) {
-  float a[8]; uint32_t u[8]; float2 p[8];
-  for (int i = 0; i < 8; ++i) { a[i] = threadIdx.x * 1.0f + i; u[i] = threadIdx.x + i; p[i] = make_float2(a[i], a[i] + 1.0f); }
+  float a[8]; uint32_t u[8]; float2 p[8]; double dd[8];
+  for (int i = 0; i < 8; ++i) { a[i] = threadIdx.x * 1.0f + i; u[i] = threadIdx.x + i; p[i] = make_float2(a[i], a[i] + 1.0f); dd[i] = a[i]; }
   asm volatile("s_mov_b64 vcc, -1\n s_mov_b64 s[20:21], -1" ::: "vcc", "s20", "s21");
   for (int it = 0; it < N_ITER; ++it) {
 #pragma unroll
@@ -70,10 +70,19 @@ template <int OP> __global__ void kern(float* out, uint32_t sv) {
       if constexpr (OP == 57) asm volatile("v_cmp_gt_f32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "vcc");
       if constexpr (OP == 58) asm volatile("v_cmp_gt_f32_e64 s[20:21], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "s20", "s21");
       if constexpr (OP == 59) asm volatile("v_cmp_gt_f32_e64 s[20:21], %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i+1)&7]), "s"(sv) : "s20", "s21");
+      if constexpr (OP == 60) asm volatile("v_add_f64 %0, %0, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 61) asm volatile("v_min_f64 %0, %0, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 62) asm volatile("v_max_f64 %0, %0, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 63) asm volatile("v_cmp_lt_f64 vcc, %0, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) : "vcc");
+      if constexpr (OP == 64) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 65) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 66) asm volatile("v_cmp_gt_f64_e64 s[20:21], 0, %0" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) : "s20", "s21");
+      if constexpr (OP == 67) asm volatile("v_add_f64 %0, %0, -%1" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
+      if constexpr (OP == 68) asm volatile("v_min_f64 %0, %0, |%1|" : "+v"(dd[i]) : "v"(dd[(i+1)&7]), "s"(sv) );
       if constexpr (OP == 43) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(p[i]) : "v"(p[(i+1)&7]), "s"(sv) );
     }
   }
-  float r = 0; for (int i = 0; i < 8; ++i) r += a[i] + p[i].x + p[i].y + (float)u[i];
+  float r = 0; for (int i = 0; i < 8; ++i) r += a[i] + p[i].x + p[i].y + (float)u[i] + (float)dd[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 template <int OP> void run(const char* name, float* out) {
@@ -85,6 +94,15 @@ template <int OP> void run(const char* name, float* out) {
   printf("%-20s ns/instr/SIMD: 1w %.3f  2w %.3f  4w %.3f\n", name, ms[0]*1e6/n, ms[1]*1e6/n/2, ms[2]*1e6/n/4);
 }
 int main() { float* out; hipMalloc(&out, 256 * 1024 * sizeof(float));
+  run<60>("v_add_f64", out);
+  run<67>("v_add_f64_neg", out);
+  run<61>("v_min_f64", out);
+  run<68>("v_min_f64_abs", out);
+  run<62>("v_max_f64", out);
+  run<63>("v_cmp_lt_f64", out);
+  run<66>("v_cmp_gt_f64_e64_0", out);
+  run<64>("v_mul_f64", out);
+  run<65>("v_fma_f64", out);
   run<0>("v_add_f32", out);
   run<1>("v_sub_f32", out);
   run<2>("v_mul_f32", out);
