@@ -26,6 +26,11 @@ VARIANTS = {
         ("                        } else if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {",
          "                        } else if constexpr (i < 0) {"),
     ]),
+    # flooding phase B in float32 with LDS atomic adds too (ds_add_f32): measured 4x slower
+    "flood_atomic_f32": (FLOOD, [
+        ("                    } else if constexpr (sizeof(T) == 8) {",
+         "                    } else if constexpr (sizeof(T) >= 4) {"),
+    ]),
     # layered pass 2: the argmin updated in place (the flooding kernel's fix for a sunk select
     # chain); here it moved 36 -> 60 B/lane of scratch and did not cut the SGPR spills
     "lay_idx_inplace": (LAYERED, [
