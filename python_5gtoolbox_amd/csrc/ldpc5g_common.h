@@ -137,6 +137,9 @@ int dec_blocks_per_cu_l(int bgn);
 int launch_dec_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
                  int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
                  hipStream_t st);
+int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                       int B, int Zc, int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha,
+                       double beta, int pc, hipStream_t st);
 int launch_dec_mixed_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
                        double beta, int pc, hipStream_t st);

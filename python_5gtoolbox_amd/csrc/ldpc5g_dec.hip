@@ -15,6 +15,10 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
                double alpha, double beta, int pc, hipStream_t st) {
     if (layered) return launch_dec_l(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    // launches whose codeblocks fit 64 slots (one small codeblock per drop-in call): 16 parts
+    const int G = std::min(dec_G(Zc, false), B);
+    if (G * Zc <= kFloodSmallCS)
+        return launch_flood_small(bgn, dtype, llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)

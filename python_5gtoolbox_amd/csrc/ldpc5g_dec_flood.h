@@ -24,7 +24,6 @@
 namespace ldpc5g_impl {
 namespace {
 
-constexpr int kFloodThreads = 2 * kDecThreads;   // two halves of 384 slots
 constexpr size_t kLdsPerCU = 160 * 1024;
 #ifndef LDPC5G_FLOOD_XPRE
 #define LDPC5G_FLOOD_XPRE 4
@@ -32,40 +31,46 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 // extension-column LLRs are loaded this many ext rows ahead of their use in phase A
 constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 
-template <int BG, typename T>
+// Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
+// state lives, and the packing of its sign word.  NP = 2, CS = 384 for batches; NP = 16, CS = 64 for
+// the small launches of the per-codeblock drop-ins (16 waves share one codeblock's rows).
+template <int BG, typename T, int NP, int CS>
 struct FloodPlan {
     int nls = 0;          // rows 0..nls-1 keep their state in LDS
-    int owner[64] = {};   // half that runs phase A of row i (and phase B of a VGPR row)
-    int slot[64] = {};    // VGPR state slot of row i in its owner half (-1: LDS row)
+    int owner[64] = {};   // part that runs phase A of row i (and phase B of a VGPR row)
+    int slot[64] = {};    // VGPR state slot of row i in its owner part (-1: LDS row)
     int nslot = 0;
     int pw[64] = {};      // VGPR sign word of row i: rows of degree <= 12 share a word (16-bit fields)
     int ph[64] = {};      // 0: whole word (negs | idx << 24), 1: low field, 2: high field (negs | idx << 12)
     int npw = 0;
     int first_row[32] = {};   // lowest base row of core column j (writes 0 + r in phase B)
-    int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner half's ext rows
-    int xlist[2][64] = {};    // ext rows of each half, ascending
-    int nx[2] = {0, 0};
+    int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner part's ext rows
+    int xlist[NP][64] = {};   // ext rows of each part, ascending
+    int nx[NP] = {};
     static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
     constexpr FloodPlan() {
         using P = BGT<BG>;
-        constexpr int CS = kDecThreads;
         const auto& G = kGroups<BG>;
         const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4;
         const int fit = (int)((kLdsPerCU - fixed) / (CS * (2 * sizeof(T) + 4)));
         int lead = 0;   // leading single-row groups: their phase B is split only if in LDS
         while (lead < G.n && G.start[lead + 1] - G.start[lead] == 1 && G.start[lead] == lead) ++lead;
         nls = fit < lead ? fit : lead;
-        int load[2] = {0, 0};
+        int load[NP] = {};
         bool done[64] = {};
+        // rows of a multi-row group on different parts (phase B balance), then every other row
+        // by decreasing degree onto the least loaded part (phase A balance)
         for (int g = 0; g < G.n; ++g) {
             if (G.start[g + 1] - G.start[g] < 2) continue;
-            int gl[2] = {0, 0};
+            int gl[NP] = {};
             for (;;) {
                 int best = -1;
                 for (int i = G.start[g]; i < G.start[g + 1]; ++i)
                     if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
                 if (best < 0) break;
-                const int h = gl[0] != gl[1] ? (gl[0] < gl[1] ? 0 : 1) : (load[0] <= load[1] ? 0 : 1);
+                int h = 0;
+                for (int q = 1; q < NP; ++q)
+                    if (gl[q] < gl[h] || (gl[q] == gl[h] && load[q] < load[h])) h = q;
                 owner[best] = h, gl[h] += deg(best), load[h] += deg(best), done[best] = true;
             }
         }
@@ -74,13 +79,15 @@ struct FloodPlan {
             for (int i = 0; i < P::MB; ++i)
                 if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
             if (best < 0) break;
-            const int h = load[0] <= load[1] ? 0 : 1;
+            int h = 0;
+            for (int q = 1; q < NP; ++q)
+                if (load[q] < load[h]) h = q;
             owner[best] = h, load[h] += deg(best), done[best] = true;
         }
-        int ns[2] = {0, 0};
+        int ns[NP] = {};
         for (int i = 0; i < P::MB; ++i) slot[i] = i < nls ? -1 : ns[owner[i]]++;
-        nslot = ns[0] > ns[1] ? ns[0] : ns[1];
-        for (int hh = 0; hh < 2; ++hh) {
+        for (int q = 0; q < NP; ++q) nslot = nslot > ns[q] ? nslot : ns[q];
+        for (int hh = 0; hh < NP; ++hh) {
             int n = 0, open = -1;
             for (int i = nls; i < P::MB; ++i) {
                 if (owner[i] != hh) continue;
@@ -106,13 +113,12 @@ struct FloodPlan {
         }
     }
 };
-template <int BG, typename T>
-constexpr FloodPlan<BG, T> kFloodPlan{};
+template <int BG, typename T, int NP, int CS>
+constexpr FloodPlan<BG, T, NP, CS> kFloodPlan{};
 
-template <int BG, typename T>
+template <int BG, typename T, int NP, int CS>
 constexpr size_t flood_lds_bytes_t() {
-    constexpr int CS = kDecThreads;
-    return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T>.nls * CS * (2 * sizeof(T) + 4) +
+    return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T, NP, CS>.nls * CS * (2 * sizeof(T) + 4) +
            (2 * kMaxG + 4) * 4;
 }
 
@@ -143,7 +149,7 @@ __device__ __forceinline__ void two_min(double& m1, double& m2, double a) {
     m1 = fmin(m1, a);
 }
 
-template <int BG, typename T, bool OFS>
+template <int BG, typename T, bool OFS, int NP, int CS>
 __device__ __forceinline__ void flood_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -151,22 +157,21 @@ __device__ __forceinline__ void flood_body(
     const CbRef* __restrict__ cbs) {
     using P = BGT<BG>;
     constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
-    constexpr int CS = kDecThreads;   // LDS column stride (entries) = slots per half
-    constexpr int NLS = kFloodPlan<BG, T>.nls;
-    constexpr int NS = kFloodPlan<BG, T>.nslot > 0 ? kFloodPlan<BG, T>.nslot : 1;
-    constexpr int NPW = kFloodPlan<BG, T>.npw > 0 ? kFloodPlan<BG, T>.npw : 1;
+    constexpr int NLS = kFloodPlan<BG, T, NP, CS>.nls;
+    constexpr int NS = kFloodPlan<BG, T, NP, CS>.nslot > 0 ? kFloodPlan<BG, T, NP, CS>.nslot : 1;
+    constexpr int NPW = kFloodPlan<BG, T, NP, CS>.npw > 0 ? kFloodPlan<BG, T, NP, CS>.npw : 1;
     constexpr int ST_B = KC * CS * TS;               // LDS rows: (mA, mB) pairs
     constexpr int PK_B = ST_B + NLS * CS * 2 * TS;   // LDS rows: sign/argmin words
     constexpr int FLAG_B = PK_B + NLS * CS * 4;
-    constexpr int KH = (KC + 1) / 2;   // own columns [0, KH) are half 0's, [KH, KC) half 1's
+    constexpr int KH = (KC + NP - 1) / NP;   // own columns [h*KH, (h+1)*KH) are part h's
     extern __shared__ __align__(16) unsigned char smem[];
 
     if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
         __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
     int Zc = Zc_u, zi = zi_u, G = G_u;
     const int t = threadIdx.x;
-    const int H = (int)(blockDim.x >> 1);   // slots per half, a multiple of 64
-    const int h = __builtin_amdgcn_readfirstlane(t >= H ? 1 : 0);
+    const int H = (int)blockDim.x / NP;   // slots per part, a multiple of 64 (<= CS)
+    const int h = __builtin_amdgcn_readfirstlane(t / H);
     const int s = t - h * H;
     if (work) {
         DecWork w = work[blockIdx.x];
@@ -236,9 +241,9 @@ __device__ __forceinline__ void flood_body(
             u = p << (32 - d), idx = p >> 24;
             asm volatile("" : "+v"(idx));   // compare idx itself with inline constants k
         } else {
-            constexpr int x = kFloodPlan<BG, T>.slot[i];
-            constexpr int w = kFloodPlan<BG, T>.pw[i];
-            constexpr int f = kFloodPlan<BG, T>.ph[i];
+            constexpr int x = kFloodPlan<BG, T, NP, CS>.slot[i];
+            constexpr int w = kFloodPlan<BG, T, NP, CS>.pw[i];
+            constexpr int f = kFloodPlan<BG, T, NP, CS>.ph[i];
             a = sA[x], b = sB[x];
             const uint32_t p = sP[w];
             if constexpr (f == 0) u = p << (32 - d), idx = p >> 24;
@@ -255,9 +260,9 @@ __device__ __forceinline__ void flood_body(
             *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + (i * CS) * 2 * TS + 2 * tzb) = v;
             *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + (i * CS) * 4 + so * 4) = negs | (idx << 24);
         } else {
-            constexpr int x = kFloodPlan<BG, T>.slot[i];
-            constexpr int w = kFloodPlan<BG, T>.pw[i];
-            constexpr int f = kFloodPlan<BG, T>.ph[i];
+            constexpr int x = kFloodPlan<BG, T, NP, CS>.slot[i];
+            constexpr int w = kFloodPlan<BG, T, NP, CS>.pw[i];
+            constexpr int f = kFloodPlan<BG, T, NP, CS>.ph[i];
             sA[x] = a, sB[x] = b;
             if constexpr (f == 0) sP[w] = negs | (idx << 24);
             else if constexpr (f == 1) sP[w] = (sP[w] & 0xffff0000u) | negs | (idx << 12);
@@ -267,7 +272,7 @@ __device__ __forceinline__ void flood_body(
 
     // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS row state 0; wrap table
     if (valid)
-        for (int j = h * KH; j < (h ? KC : KH); ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+        for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
     for (int w = t; w < NLS * CS; w += (int)blockDim.x) {
         V2<T> v;
         v.x = T(0), v.y = T(0);
@@ -292,8 +297,9 @@ __device__ __forceinline__ void flood_body(
     // f(integral_constant<half>): each half's rows form one basic block, so the scheduler can
     // overlap a row's LDS reads with the previous row's arithmetic
     auto per_half = [&](auto&& f) {
-        if (h == 0) f(std::integral_constant<int, 0>{});
-        else f(std::integral_constant<int, 1>{});
+        sfor<0, NP>([&](auto pc_) {
+            if (h == decltype(pc_)::value) f(pc_);
+        });
     };
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
     asm volatile("" : "+v"(mv));
@@ -320,8 +326,8 @@ __device__ __forceinline__ void flood_body(
         T xr[XP];
         auto xload = [&](auto hc, auto pc_) {
             constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
-            if constexpr (kXPre > 0 && p < kFloodPlan<BG, T>.nx[hh])
-                xr[p % XP] = llrx(kFloodPlan<BG, T>.xlist[hh][p]);
+            if constexpr (kXPre > 0 && p < kFloodPlan<BG, T, NP, CS>.nx[hh])
+                xr[p % XP] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][p]);
         };
         // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202)
         auto rowA = [&](auto ic) {
@@ -343,7 +349,7 @@ __device__ __forceinline__ void flood_body(
                 if constexpr (j < KC) {
                     a = at(j * CS * TS + rot(sh(e0 + k)));
                 } else {
-                    constexpr int hh = kFloodPlan<BG, T>.owner[i], p = kFloodPlan<BG, T>.xpos[i];
+                    constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
                     if constexpr (kXPre > 0) {
                         a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
                         xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
@@ -375,7 +381,7 @@ __device__ __forceinline__ void flood_body(
             per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
             sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
                 constexpr int i = decltype(ic)::value;
-                if (h == kFloodPlan<BG, T>.owner[i]) rowA(ic);
+                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) rowA(ic);
             });
             if (fail) flagA[cl] = 1;
         }
@@ -403,11 +409,11 @@ __device__ __forceinline__ void flood_body(
         prefetch_state(std::integral_constant<int, 0>{});
         // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
         if (active && flagA[cl] == 0) {
-            for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
+            for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
             per_half([&](auto hc) {
                 sfor<4, MB>([&](auto ic) {
                     constexpr int i = decltype(ic)::value;
-                    if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value)
+                    if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
                         crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
                 });
             });
@@ -429,10 +435,10 @@ __device__ __forceinline__ void flood_body(
                     for (int kk = 0; kk < k; ++kk) n += P::COL[e0 + kk] < KC;
                     return n;
                 }();
-                if constexpr (j < KC && (split < 0 || (cidx & 1) == split)) {
+                if constexpr (j < KC && (split < 0 || cidx % NP == split)) {
                     const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
                     lds_T& acc = at(j * CS * TS + rot(gshift(e0 + k)));
-                    if constexpr (kFloodPlan<BG, T>.first_row[j] == i) {
+                    if constexpr (kFloodPlan<BG, T, NP, CS>.first_row[j] == i) {
                         acc = T(0) + r;
                     } else if constexpr (sizeof(T) == 8) {
                         // ds_add_f64 without return: the LDS unit does the read-add-write (same
@@ -476,7 +482,7 @@ __device__ __forceinline__ void flood_body(
                         constexpr int i = decltype(ic)::value;
                         if constexpr (i < NLS) {   // LDS state: both halves, alternate edges
                             rowB(ic, hc, gshift, cA, cB, cu, cidx);
-                        } else if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {
+                        } else if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
                             T a, b;
                             uint32_t u, x;
                             get_state(ic, a, b, u, x);
@@ -519,7 +525,7 @@ __device__ __forceinline__ void flood_body(
                 constexpr int i = decltype(ic)::value;
                 constexpr int e0 = P::RS[i];
                 constexpr int d = P::RS[i + 1] - e0;
-                if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {
+                if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
                     bool par = false;
                     sfor<0, d>([&](auto kc) {
                         constexpr int k = decltype(kc)::value;
@@ -537,12 +543,12 @@ __device__ __forceinline__ void flood_body(
     }
     lds_barrier();
     if (active) {
-        for (int j = h * KH; j < (h ? KC : KH); ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+        for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
         per_half([&](auto hc) {
             sfor<4, MB>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
                 constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
-                if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value)
+                if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
                     crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
             });
         });
@@ -553,43 +559,57 @@ __device__ __forceinline__ void flood_body(
     }
 }
 
-template <int BG, typename T, bool OFS>
-__global__ __launch_bounds__(kFloodThreads) __attribute__((amdgpu_waves_per_eu(3))) void
+// NP parts x CS slots: 768 threads (3 waves per SIMD) for batches, 1024 (4 per SIMD) for the
+// 16-part configuration of small launches
+template <int BG, typename T, bool OFS, int NP, int CS>
+__global__ __launch_bounds__(NP * CS) __attribute__((amdgpu_waves_per_eu(NP * CS / 256))) void
 ldpc_flood_kernel(LDPC5G_DEC_PARAMS) {
-    flood_body<BG, T, OFS>(LDPC5G_DEC_ARGS);
+    flood_body<BG, T, OFS, NP, CS>(LDPC5G_DEC_ARGS);
 }
 
-template <int BG, typename T, bool OFS>
-constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS>; }
+template <int BG, typename T, bool OFS, int NP, int CS>
+constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS>; }
 
-template <int BG, typename T>
+template <int BG, typename T, int NP, int CS>
 size_t flood_lds_bytes() {
-    static_assert(flood_lds_bytes_t<BG, T>() <= kLdsPerCU, "LDS budget of one CU");
-    return flood_lds_bytes_t<BG, T>();
+    static_assert(flood_lds_bytes_t<BG, T, NP, CS>() <= kLdsPerCU, "LDS budget of one CU");
+    return flood_lds_bytes_t<BG, T, NP, CS>();
 }
 
-template <int BG, typename T>
+template <int BG, typename T, int NP, int CS>
 int set_flood_lds(bool ofs) {
-    const size_t lds = flood_lds_bytes<BG, T>();
-    return ofs ? set_lds_once<flood_kernel<BG, T, true>()>(lds)
-               : set_lds_once<flood_kernel<BG, T, false>()>(lds);
+    const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
+    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS>()>(lds)
+               : set_lds_once<flood_kernel<BG, T, false, NP, CS>()>(lds);
 }
+
+// G codeblocks per workgroup (G * Zc <= CS); NP parts of H = G*Zc rounded up to a wave
+template <int BG, typename T, int NP, int CS>
+int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                     int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                     hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS> : ldpc_flood_kernel<BG, T, false, NP, CS>;
+    const int H = ((G * Zc + 63) / 64) * 64;
+    if (G < 1 || H > CS) return fail(LDPC5G_ESIZE, "flooding launch: %d codeblocks of Zc=%d per workgroup", G, Zc);
+    if (int rc = set_flood_lds<BG, T, NP, CS>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
+    hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(NP * H), lds, st, llr, ck, status, iters, B, Zc,
+                       zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
+                       (const CbRef*)nullptr);
+    return check_hip(hipGetLastError(), "ldpc_flood_kernel launch");
+}
+
+constexpr int kFloodNP = 2, kFloodCS = kDecThreads;   // batch configuration: 2 x 384 slots
+constexpr int kFloodSmallNP = 16, kFloodSmallCS = 64;  // small launches: 16 x 64 slots
 
 template <int BG, typename T>
 int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                    int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
-    const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true> : ldpc_flood_kernel<BG, T, false>;
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks
     const int G = std::min(dec_G(Zc, false), B);
-    const int H = ((G * Zc + 63) / 64) * 64;
-    const int grid = (B + G - 1) / G;
-    if (int rc = set_flood_lds<BG, T>(ofs)) return rc;
-    const size_t lds = flood_lds_bytes<BG, T>();
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(2 * H), lds, st, llr, ck, status,
-                       iters, B, Zc, zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc,
-                       (const DecWork*)nullptr, (const CbRef*)nullptr);
-    return check_hip(hipGetLastError(), "ldpc_flood_kernel launch");
+    return launch_flood_cfg<BG, T, kFloodNP, kFloodCS>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
+                                                       alpha, beta, pc, st);
 }
 
 template <int BG, typename T>
@@ -597,22 +617,22 @@ int launch_flood_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* ite
                          const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                          int pc, hipStream_t st) {
     const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true> : ldpc_flood_kernel<BG, T, false>;
-    if (int rc = set_flood_lds<BG, T>(ofs)) return rc;
-    const size_t lds = flood_lds_bytes<BG, T>();
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodThreads), lds, st, llr, ck,
-                       status, iters, 0, 0, 0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc,
-                       work, cbs);
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS>
+                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS>;
+    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodNP * kFloodCS), lds, st, llr, ck, status, iters, 0, 0,
+                       0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
     return check_hip(hipGetLastError(), "ldpc_flood_kernel(mixed) launch");
 }
 
 template <int BG, typename T>
 int flood_blocks_per_cu_t() {
-    const size_t lds = flood_lds_bytes<BG, T>();
-    if (set_lds_once<flood_kernel<BG, T, false>()>(lds)) return -1;
+    const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
+    if (set_lds_once<flood_kernel<BG, T, false, kFloodNP, kFloodCS>()>(lds)) return -1;
     int n = -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ldpc_flood_kernel<BG, T, false>, kFloodThreads, lds) !=
-        hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS>,
+                                                     kFloodNP * kFloodCS, lds) != hipSuccess)
         return -1;
     return n;
 }

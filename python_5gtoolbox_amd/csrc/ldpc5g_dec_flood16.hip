@@ -1,0 +1,23 @@
+// ldpc5g_dec_flood16.hip — the flooding decoder's small-launch configuration: 16 parts x 64 slots
+// (1024 threads) share the base rows of at most 64 slots' codeblocks, e.g. ONE BG2 Zc=8 codeblock
+// per call from the per-codeblock drop-ins (BASELINE config 1), where the batch configuration's two
+// parts leave each wave a long serial row chain.  Own translation unit: compiles in parallel.
+#include "ldpc5g_dec_flood.h"
+
+namespace ldpc5g_impl {
+
+int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                       int B, int Zc, int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha,
+                       double beta, int pc, hipStream_t st) {
+    constexpr int NP = kFloodSmallNP, CS = kFloodSmallCS;
+    if (dtype == LDPC5G_F64) {
+        const double* p = (const double*)llr;
+        return bgn == 1 ? launch_flood_cfg<1, double, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st)
+                        : launch_flood_cfg<2, double, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
+    }
+    const float* p = (const float*)llr;
+    return bgn == 1 ? launch_flood_cfg<1, float, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st)
+                    : launch_flood_cfg<2, float, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
+}
+
+}  // namespace ldpc5g_impl

@@ -154,6 +154,25 @@ def test_decode_packed_workgroups(torch, dec, bg, Zc, schedule):
     assert got[1].sum() > 0 and len(np.unique(got[2])) > 2   # early exits at different iterations
 
 
+@pytest.mark.parametrize("bg,Zc,B", [(1, 16, 4), (2, 12, 5), (1, 64, 1), (2, 2, 32), (2, 8, 1), (1, 20, 3)])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_decode_flooding_small_launch(torch, dec, bg, Zc, B, dtype):
+    """Launches whose codeblocks fit 64 slots run the 16-part flooding configuration
+    (ldpc5g_dec_flood16.hip): bit-exact with the oracle for 1..32 codeblocks, early exits included."""
+    assert B * Zc <= 64
+    rng = np.random.default_rng(Zc * 31 + B)
+    K = (22 if bg == 1 else 10) * Zc
+    ck = rng.integers(0, 2, (B, K)).astype(np.int8)
+    snr = rng.uniform(-2.0, 3.0, (B, 1))
+    dn = O.encode(ck, bg)
+    llr = ((2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
+            10 ** (-snr / 10))).astype(dtype)
+    got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 10, "min-sum", 0.75, 0.25, "flooding")
+    ref = O.decode_flooding(llr, Zc, bg, 10, 0.75, 0.25, dtype)
+    for g, r in zip(got, ref):
+        assert np.array_equal(g, r)
+
+
 @pytest.mark.parametrize("schedule", ["flooding", "layered"])
 def test_decode_z384_batch_vs_oracle(torch, dec, schedule):
     """BASELINE config 3 shape (BG1 Zc=384, NMS alpha=0.75, L=8) on 48 codeblocks vs oracle."""
