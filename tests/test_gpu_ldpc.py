@@ -173,19 +173,21 @@ def test_decode_flooding_small_launch(torch, dec, bg, Zc, B, dtype):
         assert np.array_equal(g, r)
 
 
-@pytest.mark.parametrize("schedule", ["flooding", "layered"])
-def test_decode_z384_batch_vs_oracle(torch, dec, schedule):
-    """BASELINE config 3 shape (BG1 Zc=384, NMS alpha=0.75, L=8) on 48 codeblocks vs oracle."""
+@pytest.mark.parametrize("schedule,dtype", [("flooding", np.float32), ("layered", np.float32),
+                                            ("flooding", np.float64)])
+def test_decode_z384_batch_vs_oracle(torch, dec, schedule, dtype):
+    """BASELINE config 3 shape (BG1 Zc=384, NMS alpha=0.75, L=8) on 48 codeblocks vs oracle
+    (float64 flooding: the reference-exact mode, bit-exact with the oracle's float64 restatement)."""
     rng = np.random.default_rng(384)
     Zc, B = 384, 48
     ck = rng.integers(0, 2, (B, 22 * Zc)).astype(np.int8)
     dn = O.encode(ck, 1)
     snr = np.repeat([-3.0, 0.0, 0.5, 1.0], B // 4)[:, None]
     llr = (2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
-           10 ** (-snr / 10)).astype(np.float32)
+           10 ** (-snr / 10)).astype(dtype)
     got = dec.nr_decode_ldpc_batch(llr, Zc, 1, 8, "min-sum", 0.75, 0.0, schedule)
     ref = (O.decode_layered(llr, Zc, 1, 8, 0.75, 0.0) if schedule == "layered"
-           else O.decode_flooding(llr, Zc, 1, 8, 0.75, 0.0, np.float32))
+           else O.decode_flooding(llr, Zc, 1, 8, 0.75, 0.0, dtype))
     for g, r in zip(got, ref):
         assert np.array_equal(g, r)
 

@@ -23,8 +23,47 @@ VARIANTS = {
     "flood_noB": (FLOOD, [
         ("                        if constexpr (i < NLS) {   // LDS state: both halves, alternate edges",
          "                        if constexpr (i < 0) {"),
-        ("                        } else if constexpr (kFloodPlan<BG, T>.owner[i] == decltype(hc)::value) {",
+        ("                        } else if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {",
          "                        } else if constexpr (i < 0) {"),
+    ]),
+    # flooding phase A: rows of degree >= 12 as two independent two-min chains (even / odd edges)
+    # merged at the row end, halving the dependent f64 min/max chain
+    "flood_split2": (FLOOD, [
+        ("""            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {""",
+         """            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            T m1b = FT<T>::inf(), m2b = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0, idxb = 0;
+            constexpr bool SPL = d >= 12;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {"""),
+        ("""                idx = aq < min1 ? (uint32_t)k : idx;
+                asm volatile("" : "+v"(idx));   // update in place: a sunk select chain keeps all
+                                                // the compare masks live (scratch spills)
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                two_min(min1, min2, aq);
+                sx ^= FT<T>::sbits(q);
+            });""",
+         """                if constexpr (SPL && (k & 1)) {
+                    idxb = aq < m1b ? (uint32_t)k : idxb;
+                    asm volatile("" : "+v"(idxb));
+                    two_min(m1b, m2b, aq);
+                } else {
+                    idx = aq < min1 ? (uint32_t)k : idx;
+                    asm volatile("" : "+v"(idx));
+                    two_min(min1, min2, aq);
+                }
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                sx ^= FT<T>::sbits(q);
+            });
+            if constexpr (SPL) {
+                const bool c = m1b < min1;
+                min2 = c ? fmin(min1, m2b) : fmin(min2, m1b);
+                min1 = c ? m1b : min1;
+                idx = c ? idxb : idx;
+            }"""),
     ]),
     # flooding phase B in float32 with LDS atomic adds too (ds_add_f32): measured 4x slower
     "flood_atomic_f32": (FLOOD, [
