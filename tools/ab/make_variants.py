@@ -13,7 +13,9 @@ import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
 
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
 CSRC = os.path.join(ROOT, "python_5gtoolbox_amd", "csrc")
 LAYERED = "ldpc5g_dec_body.h"
 FLOOD = "ldpc5g_dec_flood.h"
@@ -77,6 +79,67 @@ VARIANTS = {
          "                idxn = isMin ? (uint32_t)k : idxn;\n                asm volatile(\"\" : \"+v\"(idxn));\n"),
     ]),
 }
+# layered per-row overheads (ISA count per iteration, r02s: 5583 VALU, 316 edges)
+_NOINIT = ("        T xlb[2][NXR] = {};", "        T xlb[2][NXR];")
+_IDXOP = ("            const uint32_t idxo = pk >> 24;\n",
+          "            uint32_t idxo = pk >> 24;\n            asm volatile(\"\" : \"+v\"(idxo));\n")
+_NOPF = [("""            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];""",
+          """            prefetch(gc);
+            uint32_t csw[NPW];
+#pragma unroll
+            for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];"""),
+         ("            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});\n"
+          "            lds_barrier();", "            lds_barrier();")]
+VARIANTS.update({
+    # xlb zero-initialised every iteration (~90 v_mov)
+    "lay_noinit": (LAYERED, [_NOINIT]),
+    # rows 0-3: the argmin compare folded into v_cmp_eq_u32_sdwa BYTE_3 + a v_mov of k per edge
+    "lay_idxop": (LAYERED, [_IDXOP]),
+    # shift words loaded after the barrier (no double buffer: fewer SGPRs, no writelane spills)
+    "lay_nopf": (LAYERED, _NOPF),
+    "lay_combo": (LAYERED, [_NOINIT, _IDXOP] + _NOPF),
+})
+
+
+def _pre(n):
+    """Rotated-address table lookups of the next row group's first row (its first n core edges)
+    issued BEFORE the row-group barrier: after the barrier the first data reads go out at once
+    instead of waiting for a table round trip while all three waves of the SIMD sit idle."""
+    return [
+        ("    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)\n",
+         f"    constexpr int kNPre = {n};\n    uint32_t pre[kNPre];\n"
+         "    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)\n"),
+        ("        auto layered_row = [&](auto ic, auto& gshift, T xl) {",
+         "        auto layered_row = [&](auto ic, auto& gshift, T xl, auto npre) {"),
+        ("                    rb[k] = (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)gshift(e0 + k) * GT);\n",
+         "                    if constexpr (k < decltype(npre)::value) rb[k] = (int)pre[k];\n"
+         "                    else rb[k] = (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)gshift(e0 + k) * GT);\n"),
+        ("                    layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));\n",
+         "                    layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0),\n"
+         "                                std::integral_constant<int, (g > 0 && i == kGroups<BG>.start[g]) ? kNPre : 0>{});\n"),
+        ("            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});\n"
+         "            lds_barrier();",
+         """            if constexpr (g + 1 < kGroups<BG>.n) {
+                prefetch(std::integral_constant<int, g + 1>{});
+                constexpr int i1 = kGroups<BG>.start[g + 1];
+                constexpr int e1 = P::RS[i1], d1 = P::RS[i1 + 1] - P::RS[i1];
+                sfor<0, kNPre>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (k < d1 && P::COL[e1 + k] < KC) {
+                        const uint32_t w = nsw[((e1 + k) >> 1) - group_w0<BG>(g + 1)];
+                        const uint32_t s = ((e1 + k) & 1) ? (w >> 16) : (w & 0xffffu);
+                        pre[k] = *(lds_u32*)(uintptr_t)(tzbT + s * GT);
+                    }
+                });
+            }
+            lds_barrier();"""),
+    ]
+
+
+VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
+                 "lay_pre12": (LAYERED, _pre(12))})
 
 
 def make(name):
@@ -92,6 +155,22 @@ def make(name):
     open(p, "w").write(s)
     out = os.path.join(ROOT, "build", "alt", name + ".so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    if target == LAYERED and name.startswith("lay"):
+        # only the layered TU instantiates the patched kernel: recompile it and link it with the
+        # product objects of every other TU (build/obj, from the current product build)
+        from python_5gtoolbox_amd import build as b
+        b.build(verbose=False)
+        od = os.path.join(ROOT, "build", "obj_alt_" + name)
+        os.makedirs(od, exist_ok=True)
+        try:
+            lay = b._compile(os.path.join(d, "ldpc5g_dec_l.hip"), False, od, d)
+        except subprocess.CalledProcessError as e:
+            return name, 1, str(e)
+        objs = [lay] + [os.path.join(b.OBJ, os.path.basename(x) + ".o") for x in b.sources()
+                        if os.path.basename(x) != "ldpc5g_dec_l.hip"]
+        r = subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", *objs, "-o", out],
+                           capture_output=True, text=True)
+        return name, r.returncode, r.stderr[-2000:]
     r = subprocess.run([sys.executable, "-m", "python_5gtoolbox_amd.build", "--csrc", d, "--out", out],
                        cwd=ROOT, capture_output=True, text=True)
     return name, r.returncode, r.stderr[-2000:]
@@ -99,6 +178,6 @@ def make(name):
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
-    with ThreadPoolExecutor(2) as ex:
+    with ThreadPoolExecutor(4) as ex:
         for name, rc, err in ex.map(make, names):
             print(name, "rc", rc, err if rc else "")
