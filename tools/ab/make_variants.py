@@ -138,6 +138,11 @@ def _pre(n):
     ]
 
 
+VARIANTS.update({
+    # one codeblock per 384-thread layered workgroup (78 KB LDS), two workgroups per CU: the row-group
+    # barriers of one workgroup overlap the other's work (full build: the mixed plan's G changes)
+    "t384": ("ldpc5g_common.h", [("constexpr int kDecThreadsL = 768;", "constexpr int kDecThreadsL = 384;")]),
+})
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
