@@ -87,3 +87,32 @@ def test_smallest_lifting_sizes_batch_vs_oracle(torch, bg):
         r = O.decode_layered(llr, Zc, bg, 8, 0.75, 0.0)
         assert np.array_equal(np.asarray(out), r[0]) and np.array_equal(np.asarray(st), r[1]) \
             and np.array_equal(np.asarray(it), r[2]), Zc
+
+
+@pytest.mark.parametrize("bg,Zc,B", [(1, 384, 3), (2, 176, 5), (1, 64, 13), (2, 8, 97), (1, 352, 1)])
+@pytest.mark.parametrize("schedule", ["layered", "flooding"])
+def test_batch_tail_slots_vs_oracle(torch, bg, Zc, B, schedule):
+    """Batches with B > G and B % G != 0 (G = codeblocks per workgroup) leave workgroup slots past
+    the end of the batch: those threads must neither decode nor read past the caller's rows.  The
+    LLRs sit in their own exactly-sized device tensor (a padded copy's tail is poisoned with NaN, so
+    a read past the batch that leaked into a real slot would change its result), and every output
+    is compared with the oracle (batch-tail row pointers)."""
+    from python_5gtoolbox_amd import nr_ldpc_decode as D
+    rng = np.random.default_rng(Zc * 13 + B)
+    K = (22 if bg == 1 else 10) * Zc
+    ck = rng.integers(0, 2, (B, K)).astype(np.int8)
+    dn = O.encode(ck, bg)
+    snr = rng.uniform(-1.0, 2.0, (B, 1))
+    llr = (2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
+           10 ** (-snr / 10)).astype(np.float32)
+    pad = torch.full((B + 4, llr.shape[1]), float("nan"), device="cuda")
+    pad[:B] = torch.from_numpy(llr).cuda()
+    exact = pad[:B].clone()
+    for x in (exact, pad[:B]):
+        got = D.nr_decode_ldpc_batch(x, Zc, bg, 10, "min-sum", 0.75, 0.0, schedule)
+        got = [g.cpu().numpy() for g in got]
+        ref = (O.decode_layered(llr, Zc, bg, 10, 0.75, 0.0) if schedule == "layered"
+               else O.decode_flooding(llr, Zc, bg, 10, 0.75, 0.0, np.float32))
+        assert np.array_equal(got[0], ref[0])
+        assert np.array_equal(got[1].astype(bool), ref[1].astype(bool))
+        assert np.array_equal(got[2], ref[2])
