@@ -143,6 +143,13 @@ VARIANTS.update({
     # barriers of one workgroup overlap the other's work (full build: the mixed plan's G changes)
     "t384": ("ldpc5g_common.h", [("constexpr int kDecThreadsL = 768;", "constexpr int kDecThreadsL = 384;")]),
 })
+VARIANTS.update({
+    # timing split (wrong results): the layered row loop without its row-group barriers — the
+    # barrier-exposed share of the launch
+    "lay_nobar": (LAYERED, [("            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});\n"
+                             "            lds_barrier();",
+                             "            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});\n")]),
+})
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
