@@ -150,6 +150,24 @@ VARIANTS.update({
                              "            lds_barrier();",
                              "            if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});\n")]),
 })
+# pass-1 two-min two edges at a time: min1' = min3(min1, x, y), min2' = min(min2, med3(min1, x, y))
+# (the second smallest of {min1 <= min2, x, y}): 3 ops per 2 edges instead of 4, same selections
+_MIN3 = [("""                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
+                const T aq = fabs(q[k]);
+                min2 = FT<T>::med3(min1, min2, aq);
+                min1 = fmin(min1, aq);
+""", """                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
+                if constexpr (k % 2 == 1) {
+                    const T x = fabs(q[k - 1]), y = fabs(q[k]);
+                    min2 = fmin(min2, FT<T>::med3(min1, x, y));
+                    min1 = fmin(fmin(min1, x), y);
+                } else if constexpr (k == d - 1) {
+                    const T aq = fabs(q[k]);
+                    min2 = FT<T>::med3(min1, min2, aq);
+                    min1 = fmin(min1, aq);
+                }
+""")]
+VARIANTS.update({"lay_min3": (LAYERED, _MIN3)})
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
