@@ -168,6 +168,26 @@ _MIN3 = [("""                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   /
                 }
 """)]
 VARIANTS.update({"lay_min3": (LAYERED, _MIN3)})
+def _xl_ahead(n):
+    """ext-column LLRs of row group g loaded n groups ahead (n + 1 buffers) instead of one: a row
+    group lasts ~1.1 us, about one L2-miss round trip under load."""
+    return [("        T xlb[2][NXR] = {};", f"        T xlb[{n + 1}][NXR] = {{}};"),
+            ("                xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];",
+             f"                xlb[g % {n + 1}][i - r0] = lrow[(KB + i - pc) * Zc + zv];"),
+            ("        prefetch_xl(std::integral_constant<int, 0>{});   // row 0 has no ext column: no load\n",
+             "".join(f"        prefetch_xl(std::integral_constant<int, {j}>{{}});\n" for j in range(n))),
+            ("            if constexpr (g + 1 < kGroups<BG>.n) prefetch_xl(std::integral_constant<int, g + 1>{});",
+             f"            if constexpr (g + {n} < kGroups<BG>.n) prefetch_xl(std::integral_constant<int, g + {n}>{{}});"),
+            ("layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));",
+             f"layered_row(ic, gshift, i >= 4 ? xlb[g % {n + 1}][i >= 4 ? i - r0 : 0] : T(0));")]
+
+
+VARIANTS.update({
+    "lay_xl2": (LAYERED, _xl_ahead(2)), "lay_xl3": (LAYERED, _xl_ahead(3)),
+    # timing split (wrong results): no ext-column LLR loads in the row loop
+    "lay_noxl": (LAYERED, [("                xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];",
+                            "                xlb[g & 1][i - r0] = T(0.5f);")]),
+})
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
