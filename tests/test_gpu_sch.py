@@ -335,3 +335,55 @@ def test_sch_multi_layered_matches_single_config_batches(torch, sch):
         assert torch.equal(r.tbblk[t, :c.B], one.tbblk[0, :c.B])
         cb0, C, _, _, _, _ = r.rows[t]
         assert torch.equal(r.iters[cb0:cb0 + C], one.iters[:C])
+
+
+def _random_sch_cases(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        A = int(rng.integers(24, 30000))
+        Qm = int(rng.choice([1, 2, 4, 6, 8]))
+        NL = int(rng.integers(1, 5))
+        R = float(rng.choice([rng.integers(30, 950), rng.uniform(30, 950)]))
+        rv = int(rng.integers(0, 4))
+        LBRM = int(rng.choice([0, A, int(A * rng.uniform(1, 4))]))
+        G = NL * Qm * int(rng.integers(max(1, A // (NL * Qm * 2)), 3 * A // (NL * Qm) + 10))
+        try:
+            O.sch_params(A, Qm, R, NL, rv, LBRM, G)
+        except AssertionError:
+            continue
+        out.append((A, Qm, R, NL, rv, LBRM, G))
+    return out
+
+
+@pytest.mark.parametrize("args", _random_sch_cases(20, seed=41))
+def test_sch_random_configs_chain_vs_oracle(torch, sch, args):
+    """Random transport-block configurations (both base graphs, fillers, limited-buffer rate
+    matching, every rv, Qm 1..8, 1-4 layers, fractional and integer R): the GPU encode chain ==
+    oracle.sch_encode, and the GPU decode chain (float64 flooding, the reference-exact mode) ==
+    the oracle chain — rate-recovered LLRs, hard decisions, CB CRCs, TB CRC and TB bits — for two
+    TBs at different SNRs."""
+    A, Qm, R, NL, rv, LBRM, G = args
+    rng = np.random.default_rng(A)
+    cfg = sch.sch_config(*args)
+    p = O.sch_params(*args)
+    T = 2
+    tb = rng.integers(0, 2, (T, A)).astype(np.int8)
+    g = sch.sch_encode_batch(torch.from_numpy(tb).cuda(), cfg).cpu().numpy()
+    for t in range(T):
+        assert np.array_equal(g[t], O.sch_encode(tb[t], *args)[:cfg.E_total]), t
+    snrs = [float(rng.uniform(2.0, 6.0)), float(rng.uniform(-2.0, 1.0))]
+    llr = np.stack([O.bpsk_awgn_llr(g[t], snrs[t], rng) for t in range(T)])
+    r = sch.sch_decode_batch(torch.from_numpy(llr).cuda(), cfg, 4, "min-sum", 0.75, 0.0, "flooding")
+    dn, ck = r.llr_dn.cpu().numpy(), r.ck.cpu().numpy()
+    tb_ok, tbblk = r.tb_ok.cpu().numpy().astype(bool), r.tbblk.cpu().numpy()
+    cb_ok = r.cb_crc_ok.cpu().numpy().astype(bool)
+    C = cfg.C
+    for t in range(T):
+        ref_dn = O.sch_raterecover(llr[t], p)
+        assert np.array_equal(dn[t * C:(t + 1) * C], ref_dn), t
+        rck, _, _ = O.decode_flooding(ref_dn, p["Zc"], p["bgn"], 4, 0.75, 0.0, np.float64)
+        assert np.array_equal(ck[t * C:(t + 1) * C], rck), t
+        ok, blk, cbok = O.sch_tb_check(rck, p)
+        assert tb_ok[t] == ok and np.array_equal(tbblk[t, :A], blk), t
+        assert np.array_equal(cb_ok[t * C:(t + 1) * C], cbok), t
