@@ -387,3 +387,37 @@ def test_sch_random_configs_chain_vs_oracle(torch, sch, args):
         ok, blk, cbok = O.sch_tb_check(rck, p)
         assert tb_ok[t] == ok and np.array_equal(tbblk[t, :A], blk), t
         assert np.array_equal(cb_ok[t * C:(t + 1) * C], cbok), t
+
+
+@pytest.mark.parametrize("seed", [43, 44, 45])
+def test_sch_multi_random_configs_vs_oracle(torch, sch, seed):
+    """Eight random per-TB configurations in ONE ldpc5g_sch_encode_multi and ONE
+    ldpc5g_sch_decode_multi call (float64 flooding): every TB's rate-matched bits, rate-recovered
+    LLRs, hard decisions, TB CRC flag and TB bits == the oracle chain run on that TB alone."""
+    rng = np.random.default_rng(seed)
+    specs = _random_sch_cases(8, seed)
+    cfgs = [sch.sch_config(*a) for a in specs]
+    T = len(specs)
+    Amax = max(a[0] for a in specs)
+    tb = np.zeros((T, Amax), np.int8)
+    for t, a in enumerate(specs):
+        tb[t, :a[0]] = rng.integers(0, 2, a[0])
+    g = sch.sch_encode_multi(torch.from_numpy(tb).cuda(), cfgs).cpu().numpy()
+    Emax = max(c.E_total for c in cfgs)
+    llr = np.zeros((T, Emax), np.float64)
+    for t, a in enumerate(specs):
+        E = cfgs[t].E_total
+        assert np.array_equal(g[t, :E], O.sch_encode(tb[t, :a[0]], *a)[:E]), t
+        llr[t, :E] = O.bpsk_awgn_llr(g[t, :E], float(rng.uniform(-1.0, 6.0)), rng)
+    r = sch.sch_decode_multi(torch.from_numpy(llr).cuda(), cfgs, 4, 0.75, 0.0, "flooding")
+    ok, tbblk = r.tb_ok.cpu().numpy().astype(bool), r.tbblk.cpu().numpy()
+    dn, ck = r.llr_dn.cpu().numpy(), r.ck.cpu().numpy()
+    for t, a in enumerate(specs):
+        p = O.sch_params(*a)
+        cb0, C, off, N, dck, nf = r.rows[t]
+        ref_dn = O.sch_raterecover(llr[t, :cfgs[t].E_total], p)
+        assert np.array_equal(dn[off:off + C * N].reshape(C, N), ref_dn), t
+        rck, _, _ = O.decode_flooding(ref_dn, p["Zc"], p["bgn"], 4, 0.75, 0.0, np.float64)
+        assert np.array_equal(ck[dck:dck + C * nf].reshape(C, nf), rck), t
+        rok, blk, _ = O.sch_tb_check(rck, p)
+        assert ok[t] == rok and np.array_equal(tbblk[t, :a[0]], blk), t
