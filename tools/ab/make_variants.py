@@ -188,6 +188,8 @@ VARIANTS.update({
     "lay_noxl": (LAYERED, [("                xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];",
                             "                xlb[g & 1][i - r0] = T(0.5f);")]),
 })
+# (IEEE mode off for the layered TU — -mno-amdgpu-ieee -fno-honor-nans, to drop the ~88
+# canonicalising v_max_f32 per iteration — crashes this compiler: "illegal VGPR to SGPR copy".)
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
@@ -209,6 +211,7 @@ def make(name):
         # only the layered TU instantiates the patched kernel: recompile it and link it with the
         # product objects of every other TU (build/obj, from the current product build)
         from python_5gtoolbox_amd import build as b
+        assert not os.environ.get("LDPC5G_EXTRA_FLAGS"), "the product objects must be built without A/B flags"
         b.build(verbose=False)
         od = os.path.join(ROOT, "build", "obj_alt_" + name)
         os.makedirs(od, exist_ok=True)
