@@ -190,6 +190,14 @@ VARIANTS.update({
 })
 # (IEEE mode off for the layered TU — -mno-amdgpu-ieee -fno-honor-nans, to drop the ~88
 # canonicalising v_max_f32 per iteration — crashes this compiler: "illegal VGPR to SGPR copy".)
+# stop-rule syndrome pass and final pass: rotated addresses from the wrap table (1 VALU + 1 LDS
+# read per edge) instead of rot()'s two SGPR-operand adds and a min
+VARIANTS.update({"lay_syntbl": (LAYERED, [
+    ("par ^= at(j * CS * TS + rot(shift_of<BG>(ziv, e0 + k))) < T(0);",
+     "par ^= at(j * CS * TS + (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)shift_of<BG>(ziv, e0 + k) * GT)) < T(0);"),
+    ("if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));",
+     "if constexpr (j < KC) a = at(j * CS * TS + (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)shift_of<BG>(zi, e0 + k) * GT));"),
+])})
 VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 

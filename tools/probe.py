@@ -52,7 +52,7 @@ def main():
                   f"{B * (K + N) / ms / 1e6:.0f} GB/s")
         else:
             dn = E.encode_ldpc_batch(ck, BG)
-            sigma = 10 ** (3.0 / 20)
+            sigma = 10 ** (-float(os.environ.get("PROBE_SNR", "-3")) / 20)   # default -3 dB
             llr = (2 * ((1 - 2 * dn.float()) + sigma * torch.randn(dn.shape, device="cuda",
                                                                      generator=g)) / sigma ** 2)
             out = (torch.empty((B, NF), dtype=torch.int8, device="cuda"),
