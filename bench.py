@@ -31,8 +31,11 @@ HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip 
 # rocprofv3 PMC summary of this code version (tools/gpu_round.sh pmc step -> tools/pmc_summary.py),
 # committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
+# exact kernel names as rocprofv3 reports them for the 4096-codeblock BG1 Zc=384 launches (the
+# flooding kernel's last two template arguments are its plan: 2 parts x 384 slots)
 DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false>",
-              "flooding": "void ldpc_flood_kernel<1, float, false>"}
+              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384>"}
+DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
 
@@ -40,10 +43,21 @@ def pmc_traffic(kernel, corrected16=False):
     """HBM bytes per launch of `kernel` (4096-codeblock batch) from the committed PMC summary,
     or None.  corrected16: FETCH_SIZE doubled for 16-B/lane streaming loads (MI355X_MICROARCH.md
     §HBM); the decoder's 4-B loads are uncalibrated and reported raw."""
+    e = pmc_entry(kernel)
+    if e is None:
+        return None
+    try:
+        return int(e["hbm_bytes_fetch16_corrected" if corrected16 else "hbm_bytes_raw"])
+    except (KeyError, ValueError, TypeError):
+        return None
+
+
+def pmc_entry(kernel):
+    """The committed PMC summary of exactly this kernel (no fuzzy match: a renamed or re-templated
+    kernel reports None until its counters are collected again)."""
     try:
         with open(PMC_SUMMARY) as f:
-            e = json.load(f)["kernels"][kernel]
-        return int(e["hbm_bytes_fetch16_corrected" if corrected16 else "hbm_bytes_raw"])
+            return json.load(f)["kernels"][kernel]
     except (OSError, KeyError, ValueError):
         return None
 
@@ -55,10 +69,10 @@ ALG_OPS_PER_EDGE = 13                                # lane-op
 def pmc_valu_insts(kernel):
     """VALU wave-instructions per launch of `kernel` (4096-codeblock batch) from the committed PMC
     summary (SQ_INSTS_VALU), or None."""
+    e = pmc_entry(kernel)
     try:
-        with open(PMC_SUMMARY) as f:
-            return float(json.load(f)["kernels"][kernel]["SQ_INSTS_VALU"])
-    except (OSError, KeyError, ValueError, TypeError):
+        return float(e["SQ_INSTS_VALU"]) if e else None
+    except (KeyError, ValueError, TypeError):
         return None
 
 
@@ -275,6 +289,7 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     from python_5gtoolbox_amd import phy
     from python_5gtoolbox_amd.sch import SchWorkspace, sch_config, sch_decode_batch, \
         sch_encode_batch
+    from python_5gtoolbox_amd.shard import decode_tbs_sharded
     A, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
     cfg = sch_config(A, Qm, R, NL, rv, A, G)
     g = torch.Generator(device=dev)
@@ -298,12 +313,28 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     nv = torch.full(sym.shape, nvar, dtype=torch.float32, device=dev)
     llr = torch.empty((T, G), dtype=torch.float32, device=dev)
 
+    last = {}
+
+    def rx_local(y_local):
+        phy.demod_descramble(y_local, nv, Qm, cinit, out=llr)
+        r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+        last["r"] = r
+        return r.tb_ok, r.tbblk
+    tm = {}
+    gather = world == 1 or dist.get_backend() == "nccl"   # gloo cannot gather device tensors
+
     def rx():
-        phy.demod_descramble(y, nv, Qm, cinit, out=llr)
-        return sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+        # this rank's TBs (round robin over T*world) -> records -> ONE RCCL gather to rank 0
+        if gather:
+            return decode_tbs_sharded(y, cfg, 8, T_total=T * world, decode_fn=rx_local, timing=tm)
+        return rx_local(y)
     wr, _ = timed(torch, dist, world, rx, steps, 2)
-    r = rx()
+    res = rx()
+    r = last["r"]
     ok = bool(torch.equal(r.tbblk[:, :A], tb))
+    if gather and rank == 0:   # rank 0's own TBs, back through pack -> gather -> unpack
+        ok = ok and bool(torch.equal(res[1][0::world][:, :A], tb)) and \
+            bool(torch.equal(res[0][0::world], r.tb_ok.to(torch.uint8)))
     return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, 256QAM, BG1 Zc=384, "
                         f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN {snr} dB",
             "tb_per_gpu": T, "codeblocks_per_tb": cfg.C,
@@ -316,7 +347,13 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
             "tx_ms_per_batch": round(wt / steps * 1e3, 4),
             "tb_crc_ok_frac": round(r.tb_ok.float().mean().item(), 4),
             "tb_bits_match": ok,
-            "mean_iterations": round(r.iters.float().mean().item(), 3)}
+            "mean_iterations": round(r.iters.float().mean().item(), 3),
+            "gather": ({"what": "TB round robin over ranks; (tb_ok, tbblk) packed into "
+                                f"{tm.get('gather_bytes', 0) // max(world, 1) // max(T, 1)}-B records, "
+                                "ONE dist.gather (RCCL) to rank 0, unpacked there — inside rx",
+                        "gather_ms": round(tm["gather_s"] * 1e3, 3),
+                        "gather_bytes": tm["gather_bytes"], "ranks": world}
+                       if tm else None)}
 
 
 def main():
@@ -326,11 +363,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cpu_res = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:   # before any GPU initialisation
+    if rank == 0 and args.cpu_seconds > 0:   # before any GPU initialisation
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        seconds = args.cpu_seconds
+        if world > 1:
+            # the other ranks share this host: a short single-process sample only
+            procs, seconds = 1, min(args.cpu_seconds, 6.0)
         if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
             procs = 1   # a profiler may have initialised the GPU already: no spawned workers
-        cpu_res = cpu_baseline(args.cpu_seconds, args.schedule, args.alpha, args.L, procs)
+        cpu_res = cpu_baseline(seconds, args.schedule, args.alpha, args.L, procs)
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
@@ -444,7 +485,8 @@ def main():
                          "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
                          "frac": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12
                                        / VALU_PEAK_TLANE, 4),
-                         "kernel": "void ldpc_flood_kernel<1, double, false>",
+                         "kernel": DEC64_KERNEL,
+                         "traffic": pmc_traffic(DEC64_KERNEL) if B == 4096 else None,
                          "hbm_achieved_GBps": round(B * DEC64_BYTES_PER_CB / f64_launch / 1e9, 2),
                          "algorithmic_bytes_per_cb": DEC64_BYTES_PER_CB,
                          "note": "same 13 lane-ops per edge-update in float64 against the "
@@ -468,7 +510,23 @@ def main():
                                              "traffic": pmc_traffic(ENC_KERNEL, True)
                                              if B == 4096 else None,
                                              "kernel": ENC_KERNEL,
-                                             "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB}}
+                                             "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB,
+                                             "note": "one 4096-codeblock launch moves 138 MB, "
+                                                     "which fits the 256 MB Infinity Cache: "
+                                                     "back-to-back launches are partly "
+                                                     "cache-assisted; hbm_resident is the rate "
+                                                     "with 4x the batch (553 MB per launch)"}}
+        del dnb
+        Bh = 4 * B                       # buffers well past the MALL: the HBM-resident rate
+        ckh = torch.randint(0, 2, (Bh, K_INFO), dtype=torch.int8, device=dev)
+        dnh = torch.empty((Bh, N_TX), dtype=torch.int8, device=dev)
+        w3h, e3h = timed(torch, dist, world, lambda: E.encode_ldpc_batch(ckh, BG, out=dnh), 20, 3)
+        ach_h = Bh * ENC_BYTES_PER_CB / (e3h / 20) / 1e9
+        ex["encode_config2"]["hbm_resident"] = {
+            "codeblocks_per_launch": Bh, "bytes_per_launch": Bh * ENC_BYTES_PER_CB,
+            "launch_ms": round(e3h / 20 * 1e3, 4), "codeblocks_per_s": round(Bh * world * 20 / w3h, 1),
+            "achieved_GBps": round(ach_h, 1), "frac": round(ach_h / HBM_PEAK_GBS, 4)}
+        del ckh, dnh
         ex["config1_per_codeblock"] = bench_config1(rank)
         tm = {}
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded

@@ -89,6 +89,31 @@ int ldpc5g_decode_bp(const double* llr, int8_t* ck, uint8_t* status, int32_t* it
                      double* scratch, int64_t scratch_elems, int32_t B, int32_t bgn, int32_t Zc,
                      int32_t L, int32_t flags, int64_t ldl, int64_t ldc, void* stream);
 
+/* ---- arbitrary parity-check matrix  <- py5gphy/ldpc/nr_ldpc_decode.py:51-143 decode_ldpc(LLRin, H,
+ * L, algo, alpha, beta) for ANY binary H (the 38.212 expansions have the specialised entry points
+ * above).  H is passed as a CSR of its rows plus a CSC of its columns (DEVICE int32 arrays):
+ *   row_ptr [M+1], col_idx [E]   edges of row m = col_idx[row_ptr[m] .. row_ptr[m+1]), columns
+ *                                ascending (np.where(H[m,:] == 1), :80-83); edges numbered row-major
+ *   col_ptr [N+1], col_edge [E], col_row [E]   entries of column n, rows ascending (np.where(
+ *                                H[:,n] == 1), :88-91): the edge id and its row
+ * algo LDPC5G_ALGO_MS: the min-sum family with the reference's zero-count branches (:178-227), any
+ * beta; LDPC5G_ALGO_BP: sum-product (:145-176); LDPC5G_ALGO_BF: bit flipping
+ * (ldpc_decoder_bit_flipping.py:5-73).  All float64, flooding, B codeblocks of N LLRs each:
+ *   llr [B][ldl] float64, ck [B][ldc] int8 (N decisions), status [B] uint8, iters [B] int32.
+ * A min-sum row of degree < 2 makes the reference raise (np.sort(...)[1]) once a check-node update
+ * runs; the kernel computes on, and the Python host raises the reference's error from iters/status.
+ * Per-codeblock state lives in LDS when it fits (ldpc5g_sparse_scratch_bytes returns 0), else in
+ * a caller DEVICE scratch of ldpc5g_sparse_scratch_bytes(B, M, N, E, algo) bytes (-1: bad args). */
+#define LDPC5G_ALGO_MS 0
+#define LDPC5G_ALGO_BP 1
+#define LDPC5G_ALGO_BF 2
+int64_t ldpc5g_sparse_scratch_bytes(int32_t B, int32_t M, int32_t N, int32_t E, int32_t algo);
+int ldpc5g_decode_sparse(const double* llr, int64_t ldl, int32_t B, int32_t M, int32_t N, int32_t E,
+                         const int32_t* row_ptr, const int32_t* col_idx, const int32_t* col_ptr,
+                         const int32_t* col_edge, const int32_t* col_row, int32_t L, int32_t algo,
+                         double alpha, double beta, int8_t* ck, int64_t ldc, uint8_t* status,
+                         int32_t* iters, void* scratch, int64_t scratch_bytes, void* stream);
+
 /* One codeblock of a mixed batch: base graph, lifting size, element offsets of its LLR row
  * (into llr_base, in elements) and of its ck row (into ck_base, in bytes). */
 typedef struct {
@@ -100,10 +125,11 @@ typedef struct {
 
 /* Decode a batch of codeblocks with heterogeneous (bgn, Zc) in at most two launches (one per
  * base graph).  `desc` is a HOST array of B descriptors; status[b] / iters[b] follow desc order.
- * The work list is built on the host, copied with a stream-ordered allocation
- * (hipMallocAsync / hipMemcpyAsync / hipFreeAsync on `stream`): asynchronous and reentrant, no
- * host synchronisation.  Repeated decodes of one batch shape should build the plan once instead
- * (ldpc5g_mixed_plan + ldpc5g_decode_ms_mixed_plan). */
+ * The work list is built on the host and copied into a stream-ordered allocation
+ * (hipMallocAsync / hipFreeAsync on `stream`) from a per-thread ring of 4 pinned staging buffers:
+ * the call returns once the copy is queued; it blocks only if the copy issued from the same slot
+ * 4 calls earlier has not completed yet.  Repeated decodes of one batch shape should build the
+ * plan once instead (ldpc5g_mixed_plan + ldpc5g_decode_ms_mixed_plan). */
 int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* llr_base,
                            int32_t llr_dtype, int8_t* ck_base, uint8_t* status, int32_t* iters,
                            int32_t L, double alpha, double beta, int32_t schedule,
@@ -216,7 +242,9 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
  * flat workspaces, TB after TB: ck rows of K_t, dn / llr_dn rows of N_t, decoder ck rows of
  * Nf_t = 68/52 Zc_t, status / iters / cb_crc_ok one entry per codeblock.  trblk [T][lda] (A_t
  * bits used), g / llr [T][ldg] (E_total_t used), tbblk [T][ldb] (B_t used).
- * sizes[7] = {ck elements, dn elements, decoder-ck elements, codeblocks, max A, max B, max E}. */
+ * sizes[7] = {ck elements, dn elements, decoder-ck elements, codeblocks, max A, max B, max E}.
+ * The per-TB geometry goes to the device like the mixed-Zc work list (stream-ordered allocation,
+ * pinned staging ring: see ldpc5g_decode_ms_mixed). */
 int ldpc5g_sch_multi_sizes(const ldpc5g_sch_cfg_t* cfgs, int32_t T, int64_t* sizes);
 int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
                             const ldpc5g_sch_cfg_t* cfgs, int32_t T, int8_t* ck, int8_t* dn,

@@ -17,6 +17,8 @@ Contents (reference file:line each restates):
   decode_layered ................. (no reference: the build's layered perf schedule)
   decode_bf ...................... py5gphy/ldpc/ldpc_decoder_bit_flipping.py:5-73
   decode_bp ...................... py5gphy/ldpc/nr_ldpc_decode.py:51-143, :145-176
+  decode_sparse .................. py5gphy/ldpc/nr_ldpc_decode.py:51-227 (any binary H, dense form),
+                                   ldpc_decoder_bit_flipping.py:5-73
   crc_encode / crc_decode ........ py5gphy/crc/crc.py:4-88
   get_Er / get_k0 / ratematch / raterecover  py5gphy/ldpc/nr_ldpc_ratematch.py:5-97,
                                               py5gphy/ldpc/nr_ldpc_raterecover.py:6-65
@@ -471,6 +473,94 @@ def decode_bp(llr, Zc, bgn, L, full=False):
         fail = _row_hd_fail(hd, g)
         ck[rem] = hd[rem]
         status[rem] = ~fail[rem]
+    return ck, status, iters
+
+
+# ------------------------------------------------------------------- arbitrary parity-check H
+def _pymax0(v):
+    """Python's max(v, 0) elementwise: 0 when 0 > v, else v (nr_ldpc_decode.py:201, :220)."""
+    return np.where(0 > v, 0.0, v)
+
+
+def decode_sparse(llr, H, L, algo="min-sum", alpha=1.0, beta=0.0):
+    """decode_ldpc(LLRin, H, L, algo, alpha, beta) (nr_ldpc_decode.py:51-143) for an ARBITRARY
+    0/1 matrix H, batched over rows of llr (B, N), float64, written as the reference writes it:
+    dense Lq / Lr, the per-row branches of _min_sum_process (:178-227) / _BP_process (:145-176),
+    LQ = LLRin + Lr.sum(axis=0) summed row by row (:126), ldpc_decoder_BF for algo='BF'
+    (ldpc_decoder_bit_flipping.py:5-73).  Small H only.
+    Returns ck (B, N) int8, status (B,) bool, iters (B,) int32.  A min-sum update on a row with
+    fewer than 2 edges raises IndexError, as the reference's np.sort(...)[1] does."""
+    H = np.asarray(H)
+    M, N = H.shape
+    Hi = (H == 1).astype(np.int64)
+    llr = np.atleast_2d(np.asarray(llr, np.float64))
+    B = llr.shape[0]
+    assert llr.shape[1] == N
+    A = [np.nonzero(Hi[m])[0] for m in range(M)]
+    ck = np.zeros((B, N), np.int8)
+    status = np.zeros(B, bool)
+    iters = np.full(B, L, np.int32)
+    if algo == "BF":
+        for b in range(B):
+            c = (llr[b] < 0).astype(np.int64)                   # LLR == 0 stays 0 (:41-43)
+            for it in range(L):
+                S = (Hi @ c) % 2
+                if not S.any():
+                    status[b], iters[b] = True, it
+                    break
+                En = (2 * S - 1) @ Hi                            # (:61)
+                c = np.where(En == En.max(), 1 - c, c)           # (:70)
+            ck[b] = c
+        return ck, status, iters
+    for b in range(B):
+        LLR = llr[b]
+        LQ = LLR.copy()
+        Lr = np.zeros((M, N))
+        Lq = Hi * LLR
+        done = False
+        for it in range(L):
+            c = (LQ < 0).astype(np.int64)
+            if not ((Hi @ c) % 2).any():
+                ck[b], status[b], iters[b], done = c, True, it, True
+                break
+            for m in range(M):
+                a = A[m]
+                q = Lq[m, a]
+                Lr[m, a] = 0.0
+                if algo == "BP":
+                    zero = np.nonzero(q == 0)[0]
+                    t = np.tanh(q / 2)
+                    if zero.size == 0:
+                        pv = np.prod(t)
+                        for k in range(a.size):
+                            x = pv / t[k]
+                            Lr[m, a[k]] = 2 * 19.07 if x >= 1 else (-2 * 19.07 if x <= -1
+                                                                     else 2 * np.arctanh(x))
+                    elif zero.size == 1:
+                        z = zero[0]
+                        Lr[m, a[z]] = np.prod(t[0:z]) * np.prod(t[z + 1:])
+                    continue
+                zero = np.nonzero(q == 0)[0]
+                if zero.size == 0:
+                    sp = np.prod(np.sign(q))
+                    srt = np.sort(np.abs(q))
+                    f1, f2 = srt[0], srt[1]                      # IndexError for degree < 2
+                    minv = np.where(np.abs(q) == f1, f2, f1)
+                    Lr[m, a] = alpha * sp * np.sign(q) * _pymax0(minv - beta)
+                elif zero.size == 1:
+                    z = zero[0]
+                    others = np.delete(q, z)
+                    if others.size == 0:
+                        raise IndexError("min-sum row with a single edge")
+                    Lr[m, a[z]] = alpha * np.prod(np.sign(others)) * _pymax0(np.min(np.abs(others)) - beta)
+            acc = Lr[0].copy()
+            for m in range(1, M):                                # Lr.sum(axis=0), row by row
+                acc = acc + Lr[m]
+            LQ = LLR + acc
+            Lq = np.where(Hi == 1, LQ[None, :] - Lr, Lq)         # (:129-131)
+        if not done:
+            c = (LQ <= 0).astype(np.int64)
+            ck[b], status[b] = c, not ((Hi @ c) % 2).any()
     return ck, status, iters
 
 

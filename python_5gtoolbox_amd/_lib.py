@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("LDPC5G_LIB") or os.path.join(HERE, "libldpc5g.so")
 F64, F32 = 0, 1
 FLOODING, LAYERED = 0, 1
 LLR_FULL = 1
+ALGO_MS, ALGO_BP, ALGO_BF = 0, 1, 2
 EBGN, EZC, ESIZE, EHIP = -1, -2, -3, -4
 
 # every symbol include/ldpc5g.h declares: name -> (restype, argtypes)
@@ -43,6 +44,14 @@ SIGNATURES = {
     "ldpc5g_decode_bp": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                     _c.c_int64, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
                                     _c.c_int32, _c.c_int64, _c.c_int64, _c.c_void_p]),
+    "ldpc5g_sparse_scratch_bytes": (_c.c_int64, [_c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
+                                                 _c.c_int32]),
+    "ldpc5g_decode_sparse": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int32, _c.c_int32, _c.c_int32,
+                                        _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_int32,
+                                        _c.c_double, _c.c_double, _c.c_void_p, _c.c_int64,
+                                        _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
+                                        _c.c_void_p]),
     "ldpc5g_crc": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int32, _c.c_int32,
                               _c.c_void_p, _c.c_void_p]),
     "ldpc5g_sch_config": (_c.c_int, [_c.c_int32, _c.c_int32, _c.c_double, _c.c_int32, _c.c_int32,

@@ -41,6 +41,55 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 namespace {
+// Pinned staging ring for small host-built plans (stage_h2d).  A hipMemcpyAsync from pageable
+// memory may return before the runtime has read the source, so plans are first copied into a
+// pinned slot; the slot is reused only after the event recorded behind its copy has completed.
+// The slots are never freed (a thread-exit destructor could run after the HIP runtime is gone).
+struct PinnedSlot {
+    void* buf = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    int dev = -1;
+    bool pending = false;
+};
+constexpr int kRing = 4;
+thread_local PinnedSlot t_ring[kRing];
+thread_local int t_next = 0;
+}  // namespace
+
+int stage_h2d(void* dst, const void* src, size_t n, hipStream_t st) {
+    if (n == 0) return LDPC5G_OK;
+    int dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    PinnedSlot& s = t_ring[t_next];
+    t_next = (t_next + 1) % kRing;
+    if (s.pending) {   // the copy queued from this slot kRing calls ago must have read it
+        if (int rc = check_hip(hipEventSynchronize(s.ev), "hipEventSynchronize(staging)")) return rc;
+        s.pending = false;
+    }
+    if (s.dev != dev && s.ev) {
+        (void)hipEventDestroy(s.ev);
+        s.ev = nullptr;
+    }
+    if (!s.ev) {
+        if (int rc = check_hip(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming), "hipEventCreate(staging)")) return rc;
+        s.dev = dev;
+    }
+    if (s.cap < n) {
+        if (s.buf) (void)hipHostFree(s.buf);
+        s.buf = nullptr, s.cap = 0;
+        const size_t cap = std::max<size_t>(n, 4096);
+        if (int rc = check_hip(hipHostMalloc(&s.buf, cap, hipHostMallocDefault), "hipHostMalloc(staging)")) return rc;
+        s.cap = cap;
+    }
+    memcpy(s.buf, src, n);
+    if (int rc = check_hip(hipMemcpyAsync(dst, s.buf, n, hipMemcpyHostToDevice, st), "hipMemcpyAsync(plan)")) return rc;
+    if (int rc = check_hip(hipEventRecord(s.ev, st), "hipEventRecord(staging)")) return rc;
+    s.pending = true;
+    return LDPC5G_OK;
+}
+
+namespace {
 // Mixed-batch plan layout (host bytes, copied verbatim to the device):
 //   MixedPlanHdr | DecWork[nw1] (BG1) | DecWork[nw2] (BG2) | CbRef[nref]
 struct MixedPlanHdr {
@@ -236,11 +285,11 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
     MixedPlanHdr h;
     memcpy(&h, host.data(), sizeof h);
     hipStream_t st = (hipStream_t)stream;
-    // stream-ordered scratch: allocated, filled, used and freed in stream order; the pageable
-    // source is staged by hipMemcpyAsync before it returns, so `host` may go out of scope
+    // stream-ordered scratch: allocated, filled (from a pinned staging slot), used and freed in
+    // stream order
     void* dev = nullptr;
     if (int rc = check_hip(hipMallocAsync(&dev, need, st), "hipMallocAsync(work list)")) return rc;
-    int rc = check_hip(hipMemcpyAsync(dev, host.data(), need, hipMemcpyHostToDevice, st), "hipMemcpyAsync(work list)");
+    int rc = stage_h2d(dev, host.data(), need, st);
     if (!rc) rc = launch_plan(h, (const unsigned char*)dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc, st);
     const int rc2 = check_hip(hipFreeAsync(dev, st), "hipFreeAsync(work list)");
     return rc ? rc : rc2;
@@ -271,6 +320,34 @@ int ldpc5g_decode_ms_mixed_plan(const void* plan_dev, const void* plan_host, con
     if (!llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
     return launch_plan(h, (const unsigned char*)plan_dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc,
                        (hipStream_t)stream);
+}
+
+int64_t ldpc5g_sparse_scratch_bytes(int32_t B, int32_t M, int32_t N, int32_t E, int32_t algo) {
+    if (B < 0 || M < 0 || N < 1 || E < 0 || algo < LDPC5G_ALGO_MS || algo > LDPC5G_ALGO_BF) return -1;
+    if (sparse_lds_bytes(M, N, E, algo)) return 0;
+    return (int64_t)B * sparse_cb_bytes(M, N, E, algo);
+}
+
+int ldpc5g_decode_sparse(const double* llr, int64_t ldl, int32_t B, int32_t M, int32_t N, int32_t E,
+                         const int32_t* row_ptr, const int32_t* col_idx, const int32_t* col_ptr,
+                         const int32_t* col_edge, const int32_t* col_row, int32_t L, int32_t algo,
+                         double alpha, double beta, int8_t* ck, int64_t ldc, uint8_t* status,
+                         int32_t* iters, void* scratch, int64_t scratch_bytes, void* stream) {
+    g_err.clear();
+    if (algo < LDPC5G_ALGO_MS || algo > LDPC5G_ALGO_BF) return fail(LDPC5G_ESIZE, "bad algo %d", algo);
+    if (B < 0 || M < 0 || N < 1 || E < 0 || L < 0 || (B > 1 && (ldl < N || ldc < N)))
+        return fail(LDPC5G_ESIZE, "bad sizes B=%d M=%d N=%d E=%d L=%d ldl=%lld ldc=%lld", B, M, N, E, L,
+                    (long long)ldl, (long long)ldc);
+    const int64_t need = ldpc5g_sparse_scratch_bytes(B, M, N, E, algo);
+    if (scratch_bytes < need)
+        return fail(LDPC5G_ESIZE, "scratch too small: %lld < %lld", (long long)scratch_bytes, (long long)need);
+    if (B == 0) return LDPC5G_OK;
+    if (!llr || !ck || !status || !iters || !row_ptr || !col_ptr || (need > 0 && !scratch) ||
+        (E > 0 && (!col_idx || !col_edge || !col_row)))
+        return fail(LDPC5G_ESIZE, "null buffer");
+    SparseH h{row_ptr, col_idx, col_ptr, col_edge, col_row, M, N, E, 0};
+    return launch_sparse(llr, ldl, h, ck, ldc, status, iters, scratch, B, L, algo, alpha, beta,
+                         (hipStream_t)stream);
 }
 
 }  // extern "C"

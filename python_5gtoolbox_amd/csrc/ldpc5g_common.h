@@ -156,4 +156,25 @@ int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* 
               hipStream_t st);
 int edges_of_bg(int bgn);
 
+// ---- arbitrary parity-check matrices (ldpc5g_sparse.hip): CSR rows (edges in ascending column
+// order) + CSC columns (entries in ascending row order: edge id and row)
+struct SparseH {
+    const int32_t* row_ptr;    // [M + 1]
+    const int32_t* col_idx;    // [E] column of edge e (edges numbered row-major)
+    const int32_t* col_ptr;    // [N + 1]
+    const int32_t* col_edge;   // [E] edge ids of column n, rows ascending
+    const int32_t* col_row;    // [E] their rows
+    int32_t M, N, E, pad;
+};
+int64_t sparse_cb_bytes(int M, int N, int E, int algo);
+size_t sparse_lds_bytes(int M, int N, int E, int algo);   // 0: the working set needs the scratch
+int launch_sparse(const double* llr, int64_t ldl, const SparseH& h, int8_t* ck, int64_t ldc,
+                  uint8_t* status, int32_t* iters, void* scratch, int B, int L, int algo,
+                  double alpha, double beta, hipStream_t st);
+
+// Host -> device copy of a small host-built plan on `st` through a per-thread ring of pinned
+// staging buffers: returns once the copy is queued; a slot is reused only after the event
+// recorded behind its previous copy has completed (ldpc5g_capi.hip).
+int stage_h2d(void* dst, const void* src, size_t n, hipStream_t st);
+
 }  // namespace ldpc5g_impl

@@ -578,7 +578,7 @@ struct SchMulti {
         memcpy(host.data(), geo.data(), gb);
         memcpy(host.data() + gb, rows.data(), rb);
         if (int rc = check_hip(hipMallocAsync(&dev, gb + rb, st), "hipMallocAsync(sch plan)")) return rc;
-        return check_hip(hipMemcpyAsync(dev, host.data(), gb + rb, hipMemcpyHostToDevice, st), "hipMemcpyAsync(sch plan)");
+        return stage_h2d(dev, host.data(), gb + rb, st);   // pinned staging slot (ldpc5g_capi.hip)
     }
     const SchGeo* dgeo() const { return (const SchGeo*)dev; }
     const RowRef* drows() const { return (const RowRef*)((const unsigned char*)dev + geo.size() * sizeof(SchGeo)); }

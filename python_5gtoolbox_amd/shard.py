@@ -86,13 +86,16 @@ def unpack_records(rec, R, nbits, bits=None, status=None, iters=None):
 
 def gather_record_blocks(torch, dist, rec, counts, rank, world, dst=0, group=None):
     """ONE dist.gather of every rank's record block (padded to the largest shard) to `dst`.
+    rank, world and dst are ranks WITHIN `group` (group_dst: the rank that allocates the gather
+    list is the one that receives, whatever group is passed).
     rec: (m, rb) uint8 with m = max(counts) rows, this rank's counts[rank] first.  Returns on dst
     the (world, m, rb) buffer (rank r's records in [r, :counts[r]]), None elsewhere."""
     assert rec.shape[0] >= max(counts)
+    assert 0 <= dst < world
     buf = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device) \
         if rank == dst else None
-    dist.gather(rec, gather_list=list(buf.unbind(0)) if buf is not None else None, dst=dst,
-                group=group)
+    dist.gather(rec, gather_list=list(buf.unbind(0)) if buf is not None else None,
+                group=group, group_dst=dst)
     return buf
 
 
@@ -122,6 +125,10 @@ def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="la
         n_total = llr.shape[0]
         lo, hi = shard_bounds(n_total, rank, world)
         llr = llr[lo:hi]
+    else:   # the caller's rows must be exactly this rank's shard_bounds range
+        lo, hi = shard_bounds(n_total, rank, world)
+        assert llr.shape[0] == hi - lo, \
+            f"rank {rank}: {llr.shape[0]} LLR rows, shard_bounds({n_total}) assigns {hi - lo}"
     if decode_fn is None:
         from .nr_ldpc_decode import nr_decode_ldpc_batch
 
@@ -135,6 +142,7 @@ def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="la
     sync()
     t1 = time.perf_counter()
     counts = [hi - lo for lo, hi in (shard_bounds(n_total, r, world) for r in range(world))]
+    assert ck.shape[0] == counts[rank] and st.shape[0] == counts[rank] and it.shape[0] == counts[rank]
     rb = record_bytes(K)
     rec = torch.empty((max(counts + [1]), rb), dtype=torch.uint8, device=llr.device)
     pack_fn(ck, K, st.to(torch.uint8), it.to(torch.int32), out=rec)
@@ -179,6 +187,10 @@ def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedul
         T_total = llr.shape[0]
         mine_idx = shard_round_robin(T_total, rank, world)
         llr = llr[mine_idx[0]::world] if mine_idx else llr[:0]
+    else:   # the caller's rows must be exactly this rank's round-robin TBs
+        n_mine = len(shard_round_robin(T_total, rank, world))
+        assert llr.shape[0] == n_mine, \
+            f"rank {rank}: {llr.shape[0]} TB rows, round robin over {T_total} assigns {n_mine}"
     if decode_fn is None:
         from .sch import sch_decode_batch
 
@@ -194,6 +206,7 @@ def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedul
     sync()
     t1 = time.perf_counter()
     counts = [len(shard_round_robin(T_total, r, world)) for r in range(world)]
+    assert tb_ok.shape[0] == counts[rank] and tbblk.shape[0] == counts[rank]
     rb = record_bytes(nb, iters=False)
     rec = torch.empty((max(counts + [1]), rb), dtype=torch.uint8, device=llr.device)
     pack_fn(tbblk, nb, tb_ok.to(torch.uint8), None, out=rec)

@@ -11,7 +11,8 @@ stopping rule is evaluated at exactly the reference's counts, so each BLER point
 same number of trials as the reference's.
 
 Results are returned (and optionally written as JSON, not pickle) in the reference's shape:
-(sim_config, test_config_list, test_results_list).
+(sim_config, test_config_list, test_results_list).  run_ldpc_simulation_fixed is the fixed-count
+variant of scripts/sim_ldpc_decoder_bf.py (200 codeblocks per SNR below 4 dB, 2000 from 4 dB).
 """
 import json
 
@@ -89,6 +90,57 @@ def bler_point(Zc, bgn, snr_db, crcpoly, algo, alpha, beta, L, gen, device, sche
             if count == TEST_LIMITS[-1]:
                 break
     return count, failed
+
+
+def bler_fixed(Zc, bgn, snr_db, crcpoly, algo, alpha, beta, L, n, gen, device, schedule="flooding",
+               batch=1000):
+    """(n, failed_count) over exactly n codeblocks: the fixed-count loop of
+    scripts/sim_ldpc_decoder_bf.py:77-98 (no stopping rule)."""
+    t = _lib.require_gpu()
+    from .nr_ldpc_decode import nr_decode_ldpc_batch
+    K, _, _ = code_dims(bgn, Zc)
+    count = failed = 0
+    while count < n:
+        b = min(batch, n - count)
+        blk, llr = gen_codeblocks(Zc, bgn, snr_db, crcpoly, b, gen, device)
+        x = llr if schedule == "flooding" else llr.float()
+        ck, _, _ = nr_decode_ldpc_batch(x, Zc, bgn, L, algo, alpha, beta, schedule)
+        failed += int((ck[:, :K] != blk).any(dim=1).sum().item())
+        count += b
+    return count, failed
+
+
+def run_ldpc_simulation_fixed(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list,
+                              L_list, snr_db_list, test_count_seed=200, filename=None, seed=0,
+                              schedule="flooding", verbose=False):
+    """The fixed-count BLER script scripts/sim_ldpc_decoder_bf.py:43-107 on the GPU: per SNR
+    total_count = test_count_seed if snr_db < 4 else 10 * test_count_seed (:77-80), same test
+    naming and result shape as run_ldpc_simulation."""
+    t = _lib.require_gpu()
+    dev = t.device("cuda", t.cuda.current_device())
+    gen = t.Generator(device=dev)
+    gen.manual_seed(seed)
+    flags, results, counts = [], [], []
+    for flag, algo, alpha, beta, L in test_configs(algo_list, alpha_list, beta_list, mixed_list,
+                                                   L_list):
+        flags.append(flag)
+        bler, cnt = [], []
+        for snr in snr_db_list:
+            total = test_count_seed if snr < 4 else test_count_seed * 10
+            n, f = bler_fixed(Zc, bgn, snr, crcpoly, algo, alpha, beta, L, total, gen, dev, schedule)
+            bler.append(f / n)
+            cnt.append([n, f])
+            if verbose:
+                print(f"finish test {flag}, snr_db={snr}, bler={f / n:2.5f}")
+        results.append(bler)
+        counts.append(cnt)
+    sim_config = {"Zc": Zc, "bgn": bgn}
+    if filename:
+        with open(filename, "w") as fh:
+            json.dump({"sim_config": sim_config, "test_config_list": flags,
+                       "test_results_list": results, "trials": counts,
+                       "snr_db_list": list(snr_db_list), "schedule": schedule}, fh, indent=1)
+    return sim_config, flags, results
 
 
 def run_ldpc_simulation(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list, L_list,

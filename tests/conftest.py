@@ -67,6 +67,30 @@ def load_algo_cases(algo):
     return out
 
 
+def load_sparse_cases():
+    """[dict(kind, H uint8 (M, N), L, algo, alpha, beta, llr float32[N], ck int8[N], status)] —
+    reference decode_ldpc(float64(llr), H, ...) on non-38.212 matrices
+    (tests/golden/sparse_golden.npz), and the nr_decode_ldpc beta < 0 cases as a second list."""
+    d = np.load(os.path.join(GOLD, "sparse_golden.npz"))
+    kinds = d["kinds"].tolist()
+    out = []
+    for i in range(d["M"].size):
+        M, N = int(d["M"][i]), int(d["N"][i])
+        H = _unpack(d["H"], d["H_off"], i, M * N).astype(np.uint8).reshape(M, N)
+        out.append(dict(kind=kinds[d["kind"][i]], H=H, L=int(d["L"][i]), algo=str(d["algo"][i]),
+                        alpha=float(d["alpha"][i]), beta=float(d["beta"][i]),
+                        llr=d["llr"][d["llr_off"][i]:d["llr_off"][i + 1]],
+                        ck=_unpack(d["ck_bits"], d["ck_off"], i, N), status=bool(d["status"][i])))
+    nr = []
+    for i, (bg, Zc) in enumerate(d["nr_meta"].tolist()):
+        Nf = (68 if bg == 1 else 52) * Zc
+        nr.append(dict(bg=bg, Zc=Zc, alpha=float(d["nr_ab"][i][0]), beta=float(d["nr_ab"][i][1]),
+                       llr=d["nr_llr"][d["nr_llr_off"][i]:d["nr_llr_off"][i + 1]],
+                       ck=_unpack(d["nr_ck"], d["nr_ck_off"], i, Nf),
+                       status=bool(d["nr_status"][i])))
+    return out, nr
+
+
 def load_json(name):
     with open(os.path.join(GOLD, name)) as f:
         return json.load(f)

@@ -18,6 +18,8 @@ the float64 widening of those float32 values so the fixtures are exact for both 
   sch_golden.npz/.json DLSCHDecode (+HARQ), ULSCH encode/decode, a config-5 DLSCHEncode TB
   demod_golden.npz     nrModulate / nrDemodulate (QPSK..256QAM) / gen_nrPRBS vectors
   decode_bf_golden.npz / decode_bp_golden.npz   nr_decode_ldpc with algo='BF' / 'BP'
+  sparse_golden.npz    decode_ldpc (nr_ldpc_decode.py:51) on random binary H (all algorithms), the
+                       bit-flipping toy H KAT shape, nr_decode_ldpc with beta < 0
 """
 import json
 import multiprocessing as mp
@@ -234,6 +236,139 @@ def gen_bf_bp(pool):
             ck_bits=np.concatenate([res[k][0] for k in idx]), ck_off=_offs([res[k][0] for k in idx]),
             status=np.array([res[k][1] for k in idx]))
         print(algo, "cases", len(idx), "status True", sum(res[k][1] for k in idx))
+
+
+# ---------------------------------------------------------------- arbitrary H (decode_ldpc)
+TOY_H = np.array([[1, 1, 0, 1, 0, 0],      # ldpc_decoder_bit_flipping.py:115-118
+                  [0, 1, 1, 0, 1, 0],
+                  [1, 0, 0, 0, 1, 1],
+                  [0, 0, 1, 1, 0, 1]])
+
+
+def gf2_nullspace(H):
+    """Basis of {x : H x = 0 mod 2} (rows of the returned array) — codewords for random H."""
+    A = (np.asarray(H) & 1).astype(np.uint8).copy()
+    M, N = A.shape
+    piv, r = [], 0
+    for c in range(N):
+        p = next((i for i in range(r, M) if A[i, c]), None)
+        if p is None:
+            continue
+        A[[r, p]] = A[[p, r]]
+        for i in range(M):
+            if i != r and A[i, c]:
+                A[i] ^= A[r]
+        piv.append(c)
+        r += 1
+        if r == M:
+            break
+    free = [c for c in range(N) if c not in piv]
+    basis = []
+    for f in free:
+        x = np.zeros(N, np.uint8)
+        x[f] = 1
+        for i, c in enumerate(piv):
+            x[c] = A[i, f]
+        basis.append(x)
+    return np.array(basis, np.uint8).reshape(-1, N)
+
+
+def _random_H(rng, M, N, wmin=2, wmax=7, dead_cols=0):
+    H = np.zeros((M, N), np.uint8)
+    live = np.arange(dead_cols, N)
+    for m in range(M):
+        w = int(rng.integers(wmin, min(wmax, live.size) + 1))
+        H[m, rng.choice(live, w, replace=False)] = 1
+    perm = rng.permutation(N)            # degree-0 columns land anywhere
+    return H[:, perm]
+
+
+def _sparse_case(args):
+    (H, L, algo, alpha, beta, llr) = args
+    _, dec = _ref()
+    ck, status = dec.decode_ldpc(llr.astype(np.float64), H, L, algo, alpha, beta)
+    return np.asarray(ck).astype(np.int8), bool(status)
+
+
+def gen_sparse(pool):
+    """decode_ldpc(LLRin, H, L, algo, alpha, beta) (nr_ldpc_decode.py:51-143) on random binary H
+    (not TS 38.212 expansions), all algorithms, plus the reference's 4x6 bit-flipping toy H with
+    every 1- and 2-bit LLR sign flip of every codeword (ldpc_decoder_bit_flipping.py:115-143), and
+    nr_decode_ldpc with a negative offset beta (decode_ldpc's literal zero branches)."""
+    rng = np.random.default_rng(4242)
+    shapes = [(6, 12), (8, 16), (10, 20), (12, 18), (15, 30), (20, 32), (24, 48), (32, 64),
+              (40, 60), (48, 96), (60, 120)]
+    abl = [(1.0, 0.0), (0.75, 0.0), (1.0, 0.5), (0.8, 0.3), (1.0, -0.25), (0.7, -0.1)]
+    cases = []          # (tag, H, L, algo, alpha, beta, llr)
+    for n in range(96):
+        M, N = shapes[n % len(shapes)]
+        H = _random_H(rng, M, N, dead_cols=int(n % 5 == 0))
+        basis = gf2_nullspace(H)
+        x = (rng.integers(0, 2, basis.shape[0]) @ basis % 2) if basis.size else np.zeros(N, np.uint8)
+        assert not ((H.astype(np.int64) @ x) % 2).any()
+        kind = n % 4
+        if kind == 3:    # integer LLRs with ties and exact zeros
+            llr = (1 - 2 * x.astype(np.float64)) * rng.integers(1, 4, N)
+            flip = rng.random(N) < 0.15
+            llr[flip] = -llr[flip]
+            llr[rng.random(N) < 0.08] = 0.0
+        else:
+            llr = bpsk_llr(x, float(rng.uniform(-1.0, 4.0)), rng)
+        llr = llr.astype(np.float32)
+        algo = ["min-sum", "min-sum", "BP", "BF"][n % 4] if n % 7 else "min-sum"
+        a, b = abl[n % len(abl)]
+        L = [1, 5, 12, 25][(n // 4) % 4]
+        cases.append(("rand", H, L, algo, a, b, llr))
+    # all-zero LLRs: LQ = 0 -> decision 0 -> syndrome 0 at the first check
+    for algo in ("min-sum", "BP", "BF"):
+        H = _random_H(rng, 10, 20)
+        cases.append(("zeros", H, 8, algo, 1.0, 0.0, np.zeros(20, np.float32)))
+    # the reference's toy KAT shape: every codeword, 1-bit and 2-bit sign flips, BF / min-sum / BP
+    cw = [x for x in (np.array([(v >> k) & 1 for k in range(6)], np.uint8) for v in range(64))
+          if not ((TOY_H @ x) % 2).any()]
+    for x in cw:
+        base = (2 * (1 - 2 * x.astype(np.float64)) / 10 ** (-255 / 10)).astype(np.float32)
+        for m in range(6):
+            for two in (False, True):
+                llr = base.copy()
+                llr[m] = -llr[m]
+                if two:
+                    llr[(m + 1) % 6] = -llr[(m + 1) % 6]
+                for algo in ("BF", "min-sum", "BP"):
+                    cases.append(("toy", TOY_H.astype(np.uint8), 8, algo, 1.0, 0.0, llr))
+    t = time.time()
+    res = pool.map(_sparse_case, [c[1:] for c in cases], chunksize=4)
+    print("sparse decode done", time.time() - t)
+    # nr_decode_ldpc with beta < 0 on the 38.212 graph (min-sum zero branches as written)
+    nr = []
+    _, dec = _ref()
+    for bg, Zc, snr, a, b in ((2, 4, 1.0, 1.0, -0.3), (1, 3, 0.5, 0.8, -0.2), (2, 6, -0.5, 0.75, -0.5)):
+        llr = _mk_awgn(rng, bg, Zc, snr)
+        _, ck, st = dec.nr_decode_ldpc(llr.astype(np.float64), Zc, bg, 8, "min-sum", a, b)
+        nr.append((bg, Zc, a, b, llr, np.asarray(ck, np.int8), bool(st)))
+    kinds = sorted(set(c[0] for c in cases))
+    np.savez_compressed(
+        os.path.join(OUT, "sparse_golden.npz"),
+        kind=np.array([kinds.index(c[0]) for c in cases], np.int8), kinds=np.array(kinds),
+        M=np.array([c[1].shape[0] for c in cases], np.int32),
+        N=np.array([c[1].shape[1] for c in cases], np.int32),
+        H=np.concatenate([np.packbits(c[1].reshape(-1)) for c in cases]),
+        H_off=_offs([np.packbits(c[1].reshape(-1)) for c in cases]),
+        L=np.array([c[2] for c in cases], np.int32),
+        algo=np.array([c[3] for c in cases]),
+        alpha=np.array([c[4] for c in cases]), beta=np.array([c[5] for c in cases]),
+        llr=np.concatenate([c[6] for c in cases]), llr_off=_offs([c[6] for c in cases]),
+        ck_bits=np.concatenate([np.packbits(r[0] == 1) for r in res]),
+        ck_off=_offs([np.packbits(r[0] == 1) for r in res]),
+        status=np.array([r[1] for r in res]),
+        nr_meta=np.array([(r[0], r[1]) for r in nr], np.int32),
+        nr_ab=np.array([(r[2], r[3]) for r in nr]),
+        nr_llr=np.concatenate([r[4] for r in nr]), nr_llr_off=_offs([r[4] for r in nr]),
+        nr_ck=np.concatenate([np.packbits(r[5] == 1) for r in nr]),
+        nr_ck_off=_offs([np.packbits(r[5] == 1) for r in nr]),
+        nr_status=np.array([r[6] for r in nr]))
+    print("sparse cases", len(cases), "status True", sum(r[1] for r in res),
+          "nr beta<0 cases", len(nr), [r[6] for r in nr])
 
 
 # --------------------------------------------------------------------------- rate matching
@@ -500,8 +635,7 @@ class _NoGlobals(__import__("pickle").Unpickler):
 
 # BLER pickles written by scripts/internal/sim_ldpc_internal.py:89-91 ([sim_config, labels,
 # bler_lists]) and the SNR lists of the scripts that wrote them (the pickles do not store them).
-# Left out: ldpc_decode_result_all.pickle and ldpc_decode_result_BF.pickle, whose BLER values are
-# not multiples of the current stopping rule's trial counts (an older harness made them).
+# Two pickles come from FIXED-COUNT harnesses instead of the stopping rule (FIXED_PIN_FILES).
 PIN_FILES = (
     [(f"NMS_search_alpha_ZC{z}_bgn{b}.pickle", "scripts/NMS_ldpc_search_best_alpha.py:13-27", [-0.5])
      for z in (8, 12, 28, 40, 72, 176, 208, 384) for b in (1, 2) if (z, b) != (384, 2)] +
@@ -513,6 +647,33 @@ PIN_FILES = (
     [("ldpc_decode_result_opt.pickle", "scripts/sim_ldpc_decoder.py:20-40 (L=32 run)", [-1.0, -0.5, 0.0, 0.5, 1.0]),
      ("ldpc_decode_result_opt_2.pickle", "scripts/sim_ldpc_decoder.py:20-40", [-1.0, -0.5, 0.0, 0.5, 1.0]),
      ("ldpc_decode_result_for_L.pickle", "scripts/sim_ldpc_decoder.py:57-81", [-1.0, -0.5, 0.0, 0.5])])
+
+
+# Fixed trial counts per SNR (no stopping rule):
+#  * ldpc_decode_result_BF.pickle — scripts/sim_ldpc_decoder_bf.py:19-33,73-98: Zc=10 BG1 'BF',
+#    L in {16,32,64}, snr 2..5.5 step 0.5, total_count = 200 if snr < 4 else 2000;
+#  * ldpc_decode_result_all.pickle — Zc=10 BG1 L=32, BP / min-sum / NMS .8,.5 / OMS .3,.1 / mixed
+#    (.8,.3) at snr -1..1 step 0.5 (the axis of out/ldpc_decode_result_all.png).  The harness that
+#    wrote it is not in the snapshot; its count per SNR is inferred as the least common denominator
+#    of that SNR's published values (every value is a whole number of failures at that count):
+#    300, 300, 1200, 4500, 4500.
+FIXED_PIN_FILES = (
+    ("ldpc_decode_result_BF.pickle", "scripts/sim_ldpc_decoder_bf.py:19-33,73-98",
+     [2.0, 2.5, 3.0, 3.5, 4.0, 4.5, 5.0, 5.5], lambda snr, col: 200 if snr < 4 else 2000),
+    ("ldpc_decode_result_all.pickle", "Zc=10 BG1 L=32 algorithm comparison (fixed counts inferred)",
+     [-1.0, -0.5, 0.0, 0.5, 1.0], lambda snr, col: _lcd(col)),
+)
+
+
+def _lcd(values):
+    """Least common denominator of the BLER values (limit 10^5): the smallest trial count at
+    which every value is a whole number of failures."""
+    from fractions import Fraction
+    from math import lcm
+    d = 1
+    for v in values:
+        d = lcm(d, Fraction(v).limit_denominator(100000).denominator)
+    return d
 
 
 def _parse_label(s):
@@ -546,12 +707,29 @@ def gen_pins():
                 pins.append({"file": "out/" + fname, "Zc": cfg["Zc"], "bgn": cfg["bgn"],
                              "label": lab, "algo": algo, "alpha": alpha, "beta": beta, "L": L,
                              "snr": snr, "bler": p, "config": src})
+    for fname, src, snrs, count in FIXED_PIN_FILES:
+        with open(os.path.join(REF, "out", fname), "rb") as fh:
+            cfg, labels, results = _NoGlobals(fh).load()
+        for k, snr in enumerate(snrs):
+            col = [bl[k] for bl in results]
+            n_ref = count(snr, col)
+            for lab, bl in zip(labels, results):
+                assert len(bl) == len(snrs), (fname, lab)
+                p = bl[k]
+                assert abs(p * n_ref - round(p * n_ref)) < 1e-6, (fname, lab, snr, p, n_ref)
+                algo, alpha, beta, L = _parse_label(lab)
+                pins.append({"file": "out/" + fname, "Zc": cfg["Zc"], "bgn": cfg["bgn"],
+                             "label": lab, "algo": algo, "alpha": alpha, "beta": beta, "L": L,
+                             "snr": snr, "bler": p, "config": src, "n_ref": n_ref,
+                             "rule": "fixed"})
     doc = {"_source": "BLER values the reference published in /root/reference/out/*.pickle "
                       "(written by scripts/internal/sim_ldpc_internal.py:89-91), read by "
                       "tests/golden/gen_golden.py gen_pins() with a no-globals unpickler; SNR "
                       "lists from the scripts named in 'config'.  Every point is per-BPSK-symbol "
                       "Es/N0 (nr_ldpc_decode.py:253-257), CRC24A, the reference's stopping rule "
-                      "(sim_ldpc_internal.py:66-77).",
+                      "(sim_ldpc_internal.py:66-77) except pins with rule 'fixed': n_ref trials "
+                      "per point (scripts/sim_ldpc_decoder_bf.py:73-98; the _all pickle's counts "
+                      "inferred per SNR, gen_golden.py FIXED_PIN_FILES).",
            "pins": pins}
     with open(os.path.join(OUT, "bler_pins.json"), "w") as f:
         json.dump(doc, f, indent=0)
@@ -562,7 +740,7 @@ if __name__ == "__main__":
     os.chdir(REF)
     sys.path.insert(0, OUT)    # oracle_shim: the build's oracle, used only to make codewords
     which = sys.argv[1:] or ["encode", "crc", "ratematch", "dlsch", "sch", "demod", "decode", "bfbp",
-                             "demod2", "config1", "pins"]
+                             "demod2", "config1", "pins", "sparse"]
     if "demod2" in which:
         gen_demod2()
     if "config1" in which:
@@ -587,3 +765,6 @@ if __name__ == "__main__":
     if "bfbp" in which:
         with mp.get_context("fork").Pool(6) as pool:
             gen_bf_bp(pool)
+    if "sparse" in which:
+        with mp.get_context("fork").Pool(6) as pool:
+            gen_sparse(pool)

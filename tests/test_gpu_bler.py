@@ -23,7 +23,13 @@ Bars:
     of row-serial min-sum (the over-estimated messages are reused within the same iteration),
     reproduced by the CPU layered oracle; those points are checked for flooding
     only, and test_layered_underattenuated_characterised records the direction.
-algo='BP' points run the float64 sum-product kernel (flooding only)."""
+algo='BP' points run the float64 sum-product kernel (flooding only).
+
+Pins with rule 'fixed' (out/ldpc_decode_result_BF.pickle: the bit-flipping curves of
+scripts/sim_ldpc_decoder_bf.py, 200 / 2000 codeblocks below / from 4 dB; out/
+ldpc_decode_result_all.pickle: BP, min-sum, NMS, OMS, mixed at Zc=10 L=32, counts 300 / 300 /
+1200 / 4500 / 4500 per SNR inferred from the values) carry their n_ref; our side runs a fixed
+max(2000, n_ref) codeblocks (rounded up to 1000s) with the same bars."""
 import math
 
 import pytest
@@ -50,10 +56,22 @@ def _attenuated(pin):
     return pin["alpha"] <= 0.8 or pin["beta"] >= 0.3
 
 
-def _tol(n, f, p_ref):
-    n_ref = _ref_trials(p_ref)
+def _n_ref(pin):
+    return pin["n_ref"] if pin.get("rule") == "fixed" else _ref_trials(pin["bler"])
+
+
+def _tol(n, f, pin):
+    p_ref, n_ref = pin["bler"], _n_ref(pin)
     q = (f + p_ref * n_ref) / (n + n_ref)
     return 4 * math.sqrt(q * (1 - q) * (1 / n + 1 / n_ref)) + 1 / min(n, n_ref)
+
+
+def test_pin_inventory():
+    """Every LDPC BLER value the reference published: 272 stopping-rule pins + 24 BF + 35 _all."""
+    from collections import Counter
+    c = Counter(p["file"] for p in PINS)
+    assert len(PINS) == 331
+    assert c["out/ldpc_decode_result_BF.pickle"] == 24 and c["out/ldpc_decode_result_all.pickle"] == 35
 
 
 def _cases(schedule):
@@ -67,27 +85,29 @@ def _cases(schedule):
 
 def _run(i, pin, schedule):
     import torch
-    from python_5gtoolbox_amd.sim_ldpc import bler_point
+    from python_5gtoolbox_amd.sim_ldpc import bler_fixed, bler_point
     dev = torch.device("cuda", 0)
     gen = torch.Generator(device=dev)
     gen.manual_seed(7919 * i + (1 if schedule == "layered" else 0))
-    n, f = bler_point(pin["Zc"], pin["bgn"], pin["snr"], "24A", pin["algo"], pin["alpha"],
-                      pin["beta"], pin["L"], gen, dev, schedule)
-    return n, f
+    args = (pin["Zc"], pin["bgn"], pin["snr"], "24A", pin["algo"], pin["alpha"], pin["beta"], pin["L"])
+    if pin.get("rule") == "fixed":
+        n = -(-max(2000, pin["n_ref"]) // 1000) * 1000
+        return bler_fixed(*args, n, gen, dev, schedule)
+    return bler_point(*args, gen, dev, schedule)
 
 
 @pytest.mark.parametrize("i,pin", _cases("flooding"))
 def test_bler_flooding_matches_reference(i, pin):
     n, f = _run(i, pin, "flooding")
     p, p_ref = f / n, pin["bler"]
-    assert abs(p - p_ref) <= _tol(n, f, p_ref), (pin, n, f, p)
+    assert abs(p - p_ref) <= _tol(n, f, pin), (pin, n, f, p)
 
 
 @pytest.mark.parametrize("i,pin", _cases("layered"))
 def test_bler_layered_at_least_reference(i, pin):
     n, f = _run(i, pin, "layered")
     p, p_ref = f / n, pin["bler"]
-    assert p - p_ref <= _tol(n, f, p_ref), (pin, n, f, p)
+    assert p - p_ref <= _tol(n, f, pin), (pin, n, f, p)
 
 
 def test_layered_underattenuated_characterised():

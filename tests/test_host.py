@@ -40,6 +40,8 @@ def test_header_constants_match_binding():
     assert int(consts["LDPC5G_FLOODING"]) == _lib.FLOODING
     assert int(consts["LDPC5G_LAYERED"]) == _lib.LAYERED
     assert int(consts["LDPC5G_LLR_FULL"]) == _lib.LLR_FULL
+    assert (int(consts["LDPC5G_ALGO_MS"]), int(consts["LDPC5G_ALGO_BP"]),
+            int(consts["LDPC5G_ALGO_BF"])) == (_lib.ALGO_MS, _lib.ALGO_BP, _lib.ALGO_BF)
     assert int(consts["LDPC5G_EBGN"]) == _lib.EBGN and int(consts["LDPC5G_EZC"]) == _lib.EZC
     assert ctypes.sizeof(_lib.CbDesc) == 24
 
@@ -63,6 +65,20 @@ def test_find_ils_abi_matches_reference_table():
     (lambda l: l.ldpc5g_decode_ms(None, 1, None, None, None, 4, 2, 1, 8, 1.0, 0.0, 0, 0,
                                   500, 520, None), _lib.EZC),
     (lambda l: l.ldpc5g_encode(None, None, 0, 1, 384, 8448, 25344, None), 0),   # empty batch
+    # sparse H: bad algo, N < 1, ldl < N, null buffers, scratch too small, empty batch
+    (lambda l: l.ldpc5g_decode_sparse(None, 6, 1, 4, 6, 12, None, None, None, None, None, 8, 3,
+                                      1.0, 0.0, None, 6, None, None, None, 0, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_sparse(None, 6, 1, 4, 0, 12, None, None, None, None, None, 8, 0,
+                                      1.0, 0.0, None, 6, None, None, None, 0, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_sparse(None, 5, 2, 4, 6, 12, None, None, None, None, None, 8, 0,
+                                      1.0, 0.0, None, 6, None, None, None, 0, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_sparse(None, 6, 1, 4, 6, 12, None, None, None, None, None, 8, 2,
+                                      1.0, 0.0, None, 6, None, None, None, 0, None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_sparse(None, 30000, 4, 15000, 30000, 90000, None, None, None, None,
+                                      None, 8, 0, 1.0, 0.0, None, 30000, None, None, None, 100,
+                                      None), _lib.ESIZE),
+    (lambda l: l.ldpc5g_decode_sparse(None, 6, 0, 4, 6, 12, None, None, None, None, None, 8, 1,
+                                      1.0, 0.0, None, 6, None, None, None, 0, None), 0),
 ])
 def test_abi_validation_without_gpu(call, code):
     """Argument checks run before any HIP call and return the documented codes."""
@@ -203,3 +219,15 @@ def test_mixed_plan_built_on_host():
 ])
 def test_pack_and_phy_validation_without_gpu(call, code):
     assert call(_lib.lib()) == code
+
+
+def test_sparse_scratch_sizing():
+    """LDS when the per-codeblock working set fits 156 KB, else (N + E) doubles per codeblock
+    (soft) / 5N + M bytes rounded to 16 (BF) of caller scratch; -1 on bad arguments."""
+    lib = _lib.lib()
+    assert lib.ldpc5g_sparse_scratch_bytes(10, 4, 6, 12, _lib.ALGO_MS) == 0
+    assert lib.ldpc5g_sparse_scratch_bytes(3, 8000, 16000, 48000, _lib.ALGO_MS) == 3 * 64000 * 8
+    assert lib.ldpc5g_sparse_scratch_bytes(3, 8000, 16000, 48000, _lib.ALGO_BF) == 0
+    assert lib.ldpc5g_sparse_scratch_bytes(2, 40000, 80000, 9, _lib.ALGO_BF) == 2 * 440000
+    assert lib.ldpc5g_sparse_scratch_bytes(1, 4, 0, 12, _lib.ALGO_MS) == -1
+    assert lib.ldpc5g_sparse_scratch_bytes(1, 4, 6, 12, 7) == -1

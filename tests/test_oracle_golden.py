@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, load_algo_cases, load_json
+from conftest import GOLD, load_algo_cases, load_json, load_sparse_cases
 from oracle import ldpc_oracle as O
 
 
@@ -210,10 +210,50 @@ def test_config1_golden_oracle():
 def test_bler_pins_complete():
     """Every LDPC BLER value the reference published is a pin (tests/golden/bler_pins.json)."""
     pins = load_json("bler_pins.json")["pins"]
-    assert len(pins) == 272
+    assert len(pins) == 272 + 24 + 35
     files = {p["file"] for p in pins}
     assert "out/ldpc_decode_result_opt.pickle" in files and "out/NMS_search_alpha_ZC384_bgn1.pickle" in files
-    assert {p["algo"] for p in pins} == {"min-sum", "BP"}
+    assert "out/ldpc_decode_result_BF.pickle" in files and "out/ldpc_decode_result_all.pickle" in files
+    assert {p["algo"] for p in pins} == {"min-sum", "BP", "BF"}
+    # fixed-count pins: BF 200 / 2000 codeblocks below / from 4 dB (sim_ldpc_decoder_bf.py:77-80)
+    bf = [p for p in pins if p["file"].endswith("_BF.pickle")]
+    assert all(p["n_ref"] == (200 if p["snr"] < 4 else 2000) for p in bf)
+    assert all(abs(p["bler"] * p["n_ref"] - round(p["bler"] * p["n_ref"])) < 1e-6 for p in pins if "n_ref" in p)
     assert any(p["alpha"] < 1 and p["beta"] > 0 for p in pins)      # mixed min-sum
     opt = [p["bler"] for p in pins if p["file"].endswith("_opt.pickle") and p["label"] == "NMS-alpha=0.7-L=32"]
     assert opt == [0.395, 0.135, 0.015, 0.0005, 0.0]                # BASELINE.md §1
+
+
+def test_decode_sparse_golden():
+    """decode_ldpc on arbitrary binary H: the dense restatement == the reference, bit for bit,
+    for min-sum (incl. negative offsets), BP and BF, incl. the bit-flipping toy H KAT shape."""
+    cases, _ = load_sparse_cases()
+    assert len(cases) >= 380
+    for k, c in enumerate(cases):
+        ck, st, _ = O.decode_sparse(c["llr"].astype(np.float64), c["H"], c["L"], c["algo"],
+                                    c["alpha"], c["beta"])
+        assert np.array_equal(ck[0], c["ck"]) and bool(st[0]) == c["status"], (k, c["kind"], c["algo"])
+
+
+def test_decode_sparse_degree_one_row_raises():
+    """_min_sum_process on a row with one edge raises (np.sort(...)[1], nr_ldpc_decode.py:191-194)
+    once a check-node update runs; a zero syndrome at the first check returns before it."""
+    H = np.array([[1, 1, 0], [0, 0, 1]])
+    with pytest.raises(IndexError):
+        O.decode_sparse(np.array([1.0, -2.0, 3.0]), H, 4)
+    ck, st, it = O.decode_sparse(np.array([1.0, 2.0, 3.0]), H, 4)
+    assert st[0] and it[0] == 0
+
+
+def test_decode_sparse_matches_flooding_on_38212_graph():
+    """On a TS 38.212 expansion the dense restatement and the edge-list flooding oracle agree."""
+    rng = np.random.default_rng(3)
+    for bg, Zc in ((2, 3), (1, 2)):
+        H = O.getH(Zc, bg)
+        K = (22 if bg == 1 else 10) * Zc
+        dn = O.encode(rng.integers(0, 2, K), bg)
+        llr = O.bpsk_awgn_llr(dn, 0.5, rng)
+        full = np.concatenate([np.zeros(2 * Zc), llr])
+        a = O.decode_sparse(full, H, 6, "min-sum", 0.8, 0.1)
+        b = O.decode_flooding(llr[None], Zc, bg, 6, 0.8, 0.1)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])

@@ -1,4 +1,4 @@
-"""CPU (gloo, world_size 2) tests of the multi-GPU sharding/gather logic.
+"""CPU (gloo, world_size 2 and 3) tests of the multi-GPU sharding/gather logic.
 
 The per-rank decode here is the oracle injected as `decode_fn` (test infrastructure); on the
 GPU box the same code path runs the HIP decoder over RCCL."""
@@ -67,6 +67,7 @@ def _worker(rank, world, port, q):
     try:
         from oracle import ldpc_oracle as O
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded, decode_tbs_sharded
+        from python_5gtoolbox_amd.shard import shard_bounds, shard_round_robin
         bg, Zc, B = 2, 13, 11                     # K = 130: not a multiple of 8 (padded bytes)
         rng = np.random.default_rng(5)           # same data on every rank (the "full batch")
         ck = rng.integers(0, 2, (B, 10 * Zc)).astype(np.int8)
@@ -90,25 +91,55 @@ def _worker(rank, world, port, q):
         tb_llr = torch.arange(T, dtype=torch.float32)[:, None].repeat(1, 3)
         tb = decode_tbs_sharded(tb_llr, {"B": nb}, 8, decode_fn=tb_dec, pack_fn=np_pack,
                                 unpack_fn=np_unpack)
+        exp_bits = (np.arange(T)[:, None] + np.arange(nb)[None, :]) % 2
+        ok = True
+        # this rank's rows passed explicitly (T_total / n_total): same results, gathered to the
+        # LAST rank; a row count that differs from the rank's assignment is refused
+        mine = shard_round_robin(T, rank, world)
+        tb2 = decode_tbs_sharded(tb_llr[mine], {"B": nb}, 8, T_total=T, decode_fn=tb_dec,
+                                 pack_fn=np_pack, unpack_fn=np_unpack, dst=world - 1)
+        if rank == world - 1:
+            ok &= tb2[0].tolist() == [1, 0, 1, 0, 1] and np.array_equal(tb2[1].numpy(), exp_bits)
+        else:
+            ok &= tb2 is None
+        lo, hi = shard_bounds(B, rank, world)
+        try:
+            extra = np.concatenate([llr[lo:hi], llr[:1]])      # one row too many on every rank
+            decode_codeblocks_sharded(torch.from_numpy(extra), Zc, bg, 8, n_total=B,
+                                      decode_fn=dec, pack_fn=np_pack, unpack_fn=np_unpack)
+            ok = False
+        except AssertionError:
+            pass
+        if world == 3:
+            # a sub-group {1, 2}: dst is a rank within it (group rank 0 = global rank 1)
+            sub = dist.new_group([1, 2])
+            if rank in (1, 2):
+                tb3 = decode_tbs_sharded(tb_llr, {"B": nb}, 8, decode_fn=tb_dec, pack_fn=np_pack,
+                                         unpack_fn=np_unpack, group=sub, dst=0)
+                if rank == 1:
+                    ok &= tb3[0].tolist() == [1, 0, 1, 0, 1] and np.array_equal(tb3[1].numpy(), exp_bits)
+                else:
+                    ok &= tb3 is None
         if rank == 0:
             rc, rs, ri = O.decode_layered(llr, Zc, bg, 8, 0.75, 0.0)
-            exp_bits = (np.arange(T)[:, None] + np.arange(nb)[None, :]) % 2
-            ok = (np.array_equal(res[0].numpy(), rc[:, :10 * Zc])
-                  and np.array_equal(res[1].numpy().astype(bool), rs)
-                  and np.array_equal(res[2].numpy(), ri)
-                  and tb[0].tolist() == [1, 0, 1, 0, 1]
-                  and np.array_equal(tb[1].numpy(), exp_bits)
-                  and timing["gather_bytes"] == world * 6 * (17 + 5))
-            q.put(ok)
+            ok &= (np.array_equal(res[0].numpy(), rc[:, :10 * Zc])
+                   and np.array_equal(res[1].numpy().astype(bool), rs)
+                   and np.array_equal(res[2].numpy(), ri)
+                   and tb[0].tolist() == [1, 0, 1, 0, 1]
+                   and np.array_equal(tb[1].numpy(), exp_bits)
+                   and timing["gather_bytes"] == world * -(-B // world) * (17 + 5))
         else:
-            q.put(res is None and tb is None)
+            ok &= res is None and tb is None
+        q.put(bool(ok))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_sharded_decode_gloo_world2():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_decode_gloo(world):
+    """world 2: even / uneven codeblock shards; world 3: 11 codeblocks as 4/4/3, 5 TBs as 2/2/1
+    round robin, gathers to rank 0, to the last rank, and within a sub-group."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -45,7 +45,7 @@ if has trace; then
       python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
       || { tail -20 "$OUT/rocprof.err"; die trace $?; }
   cd "$ROOT"
-  python tools/rocpd_summary.py "$OUT/prof_headline" > "$OUT/kernel_stats_headline.csv"
+  python tools/rocpd_summary.py "$OUT/prof_headline" --skip 3 > "$OUT/kernel_stats_headline.csv"
   python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
   cut -c1-150 "$OUT/kernel_stats_headline.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
