@@ -32,10 +32,11 @@ HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip 
 # committed: FETCH_SIZE / WRITE_SIZE per launch cannot be collected inside the timed run.
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 # exact kernel names as rocprofv3 reports them for the 4096-codeblock BG1 Zc=384 launches (the
-# flooding kernel's last two template arguments are its plan: 2 parts x 384 slots)
-DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false>",
-              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384>"}
-DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384>"
+# flooding kernel's 4th/5th template arguments are its plan: 2 parts x 384 slots; the last one of
+# both kernels is DEAD, the LDPC5G_RATE_MATCHED variant, false for the headline)
+DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false, false>",
+              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false>"}
+DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384, false>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
 
@@ -269,10 +270,12 @@ def bench_config4(torch, dist, world, dev, rank, steps):
             info_bits += n_per * K
     mb = MixedBatch(groups)
     B = mb.B
-    wall, _ = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered"), steps, 2)
-    _, st, it = mb.decode(8, 1.0, 0.5, "layered")
+    # rate-recovered rows: untransmitted parity columns are +0.0 (LDPC5G_RATE_MATCHED)
+    wall, _ = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered", True), steps, 2)
+    _, st, it = mb.decode(8, 1.0, 0.5, "layered", True)
     return {"workload": "BASELINE config 4: 12 (Zc, BG) groups x 341 CBs, random (Qm, rv, E), "
-                        "GPU rate match/recover, snr 1 dB, layered OMS beta=0.5 L=8",
+                        "GPU rate match/recover, snr 1 dB, layered OMS beta=0.5 L=8, "
+                        "LDPC5G_RATE_MATCHED",
             "codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
             "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
             "ms_per_call": round(wall / steps * 1e3, 4),

@@ -42,6 +42,12 @@ extern "C" {
 /* decode flags */
 #define LDPC5G_LLR_FULL 1  /* LLR rows hold all Nf = 68Zc/52Zc columns, the 2Zc punctured ones
                               included (decode_ldpc(LLRin, H, ...) input, nr_ldpc_decode.py:51) */
+#define LDPC5G_RATE_MATCHED 2  /* LLR rows come from rate recovery (nr_ldpc_raterecover.py:6-65):
+                              extension columns that were never transmitted hold +0.0.  The
+                              decoder detects rows whose extension column is +0.0 in every
+                              codeblock of a workgroup and skips their (provably null) updates;
+                              results are bit-identical to the plain decode.  Ignored by launches
+                              of <= 64 codeblock slots (one small codeblock) and by BF / BP. */
 
 /* decoding schedules */
 #define LDPC5G_FLOODING 0  /* the reference's two-phase (Jacobi) schedule, nr_ldpc_decode.py:105-131 */

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("LDPC5G_LIB") or os.path.join(HERE, "libldpc5g.so")
 F64, F32 = 0, 1
 FLOODING, LAYERED = 0, 1
 LLR_FULL = 1
+RATE_MATCHED = 2   # LDPC5G_RATE_MATCHED: rate-recovered rows, untransmitted columns +0.0
 ALGO_MS, ALGO_BP, ALGO_BF = 0, 1, 2
 EBGN, EZC, ESIZE, EHIP = -1, -2, -3, -4
 

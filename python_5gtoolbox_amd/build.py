@@ -28,7 +28,7 @@ FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-f
 # v_pk_add_f32 issues at ~1/3 the rate of two scalar v_add_f32 on gfx950 (tools/microbench/valu_rates.hip),
 # so the layered decoder TU is built without the SLP vectorizer that forms it (the flooding TU keeps
 # it: there the packed adds measure faster).
-NO_SLP = {"ldpc5g_dec_l.hip"}
+NO_SLP = {"ldpc5g_dec_l.hip", "ldpc5g_dec_l_dead.hip"}
 
 
 def sources():
@@ -59,6 +59,23 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
+def _obj_fresh(obj, cmd):
+    """The object exists, was built by exactly `cmd`, and is newer than every file its
+    dependency list (hipcc -MMD) names."""
+    try:
+        with open(obj + ".cmd") as f:
+            if f.read() != " ".join(cmd):
+                return False
+        with open(obj + ".d") as f:
+            text = f.read().replace("\\\n", " ")
+        t = os.path.getmtime(obj)
+    except OSError:
+        return False
+    deps_ = text.split(":", 1)[1].split() if ":" in text else []
+    return bool(deps_) and all(os.path.getmtime(d) <= t for d in deps_ if os.path.exists(d)) and \
+        all(os.path.exists(d) for d in deps_)
+
+
 def _compile(src, verbose, obj_dir=None, csrc=CSRC):
     obj = os.path.join(obj_dir or OBJ, os.path.basename(src) + ".o")
     flags = [f for f in FLAGS if f != f"-I{CSRC}"] + [f"-I{csrc}"]
@@ -66,9 +83,13 @@ def _compile(src, verbose, obj_dir=None, csrc=CSRC):
     if os.path.basename(src) in NO_SLP and not os.environ.get("LDPC5G_SLP"):
         flags.append("-fno-slp-vectorize")
     cmd = [HIPCC, *flags, "-c", src, "-o", obj]
+    if _obj_fresh(obj, cmd):   # incremental: only translation units whose inputs changed
+        return obj
     if verbose:
         print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    subprocess.run(cmd + ["-MMD", "-MF", obj + ".d"], check=True)
+    with open(obj + ".cmd", "w") as f:
+        f.write(" ".join(cmd))
     return obj
 
 
@@ -110,19 +131,34 @@ def asan_runtime():
     return p
 
 
+ASAN_SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+            "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+
+def _asan_stamp():
+    return " ".join([HIPCC, ARCH, *FLAGS, *ASAN_SAN, *sorted(NO_SLP)])
+
+
 def build_asan(force=False, verbose=False):
     """Host-code sanitizer build: every TU's HOST code compiled with
     AddressSanitizer + UndefinedBehaviorSanitizer (-Xarch_host: the device code is the normal
-    gfx950 build), into build/asan/libldpc5g.so.  It backs the CPU suite's
-    validation / plan-building / configuration tests (tests/test_asan_host.py), which exercise
-    exactly the C-ABI host code: argument checks, ldpc5g_sch_config, the mixed-Zc and per-TB plans."""
+    gfx950 build, which the host registration code needs), into build/asan/libldpc5g.so, per
+    translation unit incrementally like build().  It backs the CPU suite's validation /
+    plan-building / configuration tests (tests/test_asan_host.py), which exercise exactly the
+    C-ABI host code: argument checks, ldpc5g_sch_config, the mixed-Zc and per-TB plans.  Built
+    lazily by that test, not by the product build()."""
     out_dir = os.path.dirname(ASAN_LIB)
-    if not force and os.path.exists(ASAN_LIB) and \
+    stamp = ASAN_LIB + ".stamp"
+    try:
+        with open(stamp) as f:
+            same = f.read() == _asan_stamp()
+    except OSError:
+        same = False
+    if not force and same and os.path.exists(ASAN_LIB) and \
             all(os.path.getmtime(d) <= os.path.getmtime(ASAN_LIB) for d in deps()):
         return ASAN_LIB
     os.makedirs(out_dir, exist_ok=True)
-    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
-           "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer"]
+    san = list(ASAN_SAN)
     base = list(FLAGS)
 
     def one(src):
@@ -130,9 +166,13 @@ def build_asan(force=False, verbose=False):
         cmd = [HIPCC, *base, *san, "-c", src, "-o", obj]
         if os.path.basename(src) in NO_SLP:
             cmd.insert(1, "-fno-slp-vectorize")
+        if not force and _obj_fresh(obj, cmd):
+            return obj
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        subprocess.run(cmd + ["-MMD", "-MF", obj + ".d"], check=True)
+        with open(obj + ".cmd", "w") as f:
+            f.write(" ".join(cmd))
         return obj
     srcs = sources()
     with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
@@ -143,6 +183,8 @@ def build_asan(force=False, verbose=False):
         print(" ".join(link), flush=True)
     subprocess.run(link, check=True)
     os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
+    with open(stamp, "w") as f:
+        f.write(_asan_stamp())
     return ASAN_LIB
 
 

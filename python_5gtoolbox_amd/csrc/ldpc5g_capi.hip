@@ -145,7 +145,7 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
 // launches of a plan (host copy `h` for the counts, device copy `dev` for the kernels)
 int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr_base, int llr_dtype,
                 int8_t* ck_base, uint8_t* status, int32_t* iters, int L, double alpha, double beta,
-                int pc, hipStream_t st) {
+                int pc, bool dead, hipStream_t st) {
     const DecWork* w1 = (const DecWork*)(dev + sizeof(MixedPlanHdr));
     const DecWork* w2 = w1 + h.nw1;
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
@@ -154,7 +154,7 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
         const int nwg = g == 0 ? h.nw1 : h.nw2;
         if (!nwg) continue;
         if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
-                                      g == 0 ? w1 : w2, r, L, alpha, beta, pc, st))
+                                      g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, st))
             return rc;
     }
     return LDPC5G_OK;
@@ -224,7 +224,7 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
     if (B == 0) return LDPC5G_OK;
     if (!llr || !ck || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
     return launch_dec(bgn, llr_dtype, schedule == LDPC5G_LAYERED, llr, ck, status, iters, B, Zc, zi,
-                      ldl, ldc, L, alpha, beta, pc, (hipStream_t)stream);
+                      ldl, ldc, L, alpha, beta, pc, (flags & LDPC5G_RATE_MATCHED) != 0, (hipStream_t)stream);
 }
 
 int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
@@ -290,7 +290,8 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
     void* dev = nullptr;
     if (int rc = check_hip(hipMallocAsync(&dev, need, st), "hipMallocAsync(work list)")) return rc;
     int rc = stage_h2d(dev, host.data(), need, st);
-    if (!rc) rc = launch_plan(h, (const unsigned char*)dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc, st);
+    if (!rc) rc = launch_plan(h, (const unsigned char*)dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc,
+                              (flags & LDPC5G_RATE_MATCHED) != 0, st);
     const int rc2 = check_hip(hipFreeAsync(dev, st), "hipFreeAsync(work list)");
     return rc ? rc : rc2;
 }
@@ -319,6 +320,7 @@ int ldpc5g_decode_ms_mixed_plan(const void* plan_dev, const void* plan_host, con
     if (h.nref == 0) return LDPC5G_OK;
     if (!llr_base || !ck_base || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
     return launch_plan(h, (const unsigned char*)plan_dev, llr_base, llr_dtype, ck_base, status, iters, L, alpha, beta, pc,
+                       (flags & LDPC5G_RATE_MATCHED) != 0,
                        (hipStream_t)stream);
 }
 

@@ -137,6 +137,19 @@ int dec_blocks_per_cu_l(int bgn);
 int launch_dec_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
                  int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
                  hipStream_t st);
+// the dead-extension-row variants (LDPC5G_RATE_MATCHED): ldpc5g_dec_l_dead.hip / ldpc5g_dec_dead.hip
+int launch_dec_l_dead(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
+                      int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta,
+                      int pc, hipStream_t st);
+int launch_dec_mixed_l_dead(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                            int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
+                            double beta, int pc, hipStream_t st);
+int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
+                      int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
+                      double alpha, double beta, int pc, hipStream_t st);
+int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
+                            int32_t* iters, int nwg, const DecWork* work, const CbRef* cbs, int L,
+                            double alpha, double beta, int pc, hipStream_t st);
 int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int B, int Zc, int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha,
                        double beta, int pc, hipStream_t st);
@@ -145,10 +158,11 @@ int launch_dec_mixed_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, i
                        double beta, int pc, hipStream_t st);
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
-               double alpha, double beta, int pc, hipStream_t st);
+               double alpha, double beta, int pc, bool dead, hipStream_t st);
 int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
                      uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
-                     const CbRef* cbs, int L, double alpha, double beta, int pc, hipStream_t st);
+                     const CbRef* cbs, int L, double alpha, double beta, int pc, bool dead,
+                     hipStream_t st);
 int launch_bf(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
               int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc, hipStream_t st);
 int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

@@ -13,12 +13,15 @@ int dec_blocks_per_cu(int bgn, int dtype, bool layered) {
 
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
-               double alpha, double beta, int pc, hipStream_t st) {
-    if (layered) return launch_dec_l(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+               double alpha, double beta, int pc, bool dead, hipStream_t st) {
+    if (layered)
+        return dead ? launch_dec_l_dead(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                    : launch_dec_l(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     // launches whose codeblocks fit 64 slots (one small codeblock per drop-in call): 16 parts
     const int G = std::min(dec_G(Zc, false), B);
     if (G * Zc <= kFloodSmallCS)
         return launch_flood_small(bgn, dtype, llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
+    if (dead) return launch_flood_dead(bgn, dtype, llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
@@ -31,8 +34,12 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
 
 int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
                      uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
-                     const CbRef* cbs, int L, double alpha, double beta, int pc, hipStream_t st) {
-    if (layered) return launch_dec_mixed_l(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+                     const CbRef* cbs, int L, double alpha, double beta, int pc, bool dead,
+                     hipStream_t st) {
+    if (layered)
+        return dead ? launch_dec_mixed_l_dead(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                    : launch_dec_mixed_l(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    if (dead) return launch_flood_mixed_dead(bgn, dtype, llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)

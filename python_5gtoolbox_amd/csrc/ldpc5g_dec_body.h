@@ -18,6 +18,7 @@ struct FT;
 template <>
 struct FT<float> {
     __device__ static __forceinline__ uint32_t sbits(float x) { return __float_as_uint(x); }
+    __device__ static __forceinline__ uint32_t bits(float x) { return __float_as_uint(x); }
     // x with its sign bit XORed by bit 31 of `b`
     __device__ static __forceinline__ float xsign(float x, uint32_t b) {
         return __uint_as_float(__float_as_uint(x) ^ (b & 0x80000000u));
@@ -30,6 +31,7 @@ struct FT<float> {
 template <>
 struct FT<double> {
     __device__ static __forceinline__ uint32_t sbits(double x) { return (uint32_t)__double2hiint(x); }
+    __device__ static __forceinline__ uint64_t bits(double x) { return (uint64_t)__double_as_longlong(x); }
     __device__ static __forceinline__ double xsign(double x, uint32_t b) {
         return __longlong_as_double(__double_as_longlong(x) ^ ((long long)(b & 0x80000000u) << 32));
     }
@@ -141,6 +143,18 @@ constexpr int max_group_ext_rows() {
     return m;
 }
 
+// Rows of group g as bits (i - 4) of an extension-row mask, or 0 when the group holds one of the
+// core rows 0..3 (those have no extension column and are never dead).
+template <int BG>
+constexpr uint64_t group_xmask(int g) {
+    uint64_t m = 0;
+    for (int i = kGroups<BG>.start[g]; i < kGroups<BG>.start[g + 1]; ++i) {
+        if (i < 4) return 0;
+        m |= 1ull << (i - 4);
+    }
+    return m;
+}
+
 // Workgroup barrier that orders LDS only.  Threads of the decoder never exchange data through
 // global memory, and __syncthreads()'s global release would make every barrier wait (vmcnt(0))
 // for the ext-LLR loads prefetched across it.
@@ -152,7 +166,9 @@ __device__ __forceinline__ void lds_barrier() {
 
 // OFS = false: the caller guarantees beta == 0 (plain / normalized min-sum), so the offset and
 // its clamp at 0 are compiled out (min >= +0 already; the result is identical).
-template <int BG, typename T, bool LAYERED, bool OFS = true>
+// DEAD = true: the variant for rate-recovered inputs (LDPC5G_RATE_MATCHED), which detects and
+// skips dead extension rows; DEAD = false compiles none of that (the headline kernel).
+template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false>
 __device__ __forceinline__ void dec_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -289,18 +305,25 @@ __device__ __forceinline__ void dec_body(
 
     uint32_t hdc_prev = 0;   // hard decisions of own core columns, last iteration end
     uint64_t hdx_prev = 0;   // ... of own extension columns
+    uint64_t nzx = 0;        // extension columns whose LLR is not +0.0 (bit pattern) at this z
     if (valid) {
         for (int j = 0; j < KC; ++j) {
             const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
             own(j) = v;
             hdc_prev |= (uint32_t)(v < T(0)) << j;
         }
-        for (int i4 = 0; i4 < MB - 4; ++i4)
-            hdx_prev |= (uint64_t)(lrow[(KB + 4 + i4 - pc) * Zc + z] < T(0)) << i4;
+        for (int i4 = 0; i4 < MB - 4; ++i4) {
+            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            hdx_prev |= (uint64_t)(v < T(0)) << i4;
+            nzx |= (uint64_t)(FT<T>::bits(v) != 0) << i4;
+        }
     }
     for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);
     if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+    uint32_t* livew = (uint32_t*)(anyf + 2);   // workgroup OR of nzx (2 words)
     if (t == 0) *anyf = 0;
+    if constexpr (DEAD)
+        if (t == 0) livew[0] = 0u, livew[1] = 0u;
     using lds_u32 = __attribute__((address_space(3))) uint32_t;
     {   // T[e] = byte offset of entry e mod (Zc*G), e in [0, 2*Zc*G)
         const int ZG = Zc * G;
@@ -312,6 +335,32 @@ __device__ __forceinline__ void dec_body(
     const uint32_t tzbT = (uint32_t)(TBL_B + (valid ? t : 0) * 4);
     bool active = valid;
     lds_barrier();
+    // Dead extension rows: a row whose degree-1 column has LLR +0.0 for every codeblock slot of the
+    // workgroup (punctured by rate matching: high code rates leave most parity columns untransmitted)
+    // sends exactly +-0 to every core column (its min |q| is the zero of the extension edge), so the
+    // core APPs never change through it; only its extension decision r_ext = sign * alpha *
+    // max(min|q_core| - beta, 0) does.  Such rows run dead_row (pass 1 without the old-message
+    // rebuild, no APP writes) and consecutive dead groups share one barrier: bit-identical results.
+    // gdm: bit g set when every row of group g is dead (a workgroup-uniform SGPR)
+    uint32_t gdm = 0;
+    if constexpr (DEAD) {
+        if (nzx & 0xffffffffu) atomicOr(&livew[0], (uint32_t)nzx);
+        if (nzx >> 32) atomicOr(&livew[1], (uint32_t)(nzx >> 32));
+        lds_barrier();
+        const uint64_t live_x = ((uint64_t)__builtin_amdgcn_readfirstlane(livew[1]) << 32) |
+                                (uint64_t)__builtin_amdgcn_readfirstlane(livew[0]);
+        sfor<0, kGroups<BG>.n>([&](auto gc) {
+            constexpr uint64_t m = group_xmask<BG>(decltype(gc)::value);
+            if constexpr (m != 0)
+                if ((live_x & m) == 0) gdm |= 1u << decltype(gc)::value;
+        });
+        gdm = __builtin_amdgcn_readfirstlane(gdm);
+    }
+    auto gdead = [&](auto gc) -> bool {
+        constexpr int g = decltype(gc)::value;
+        if constexpr (!DEAD || group_xmask<BG>(g) == 0) return false;
+        else return (gdm >> g) & 1u;
+    };
 
     // byte offset (without the column base) of column entry (z + s) mod Zc of this thread
     // ((z + s) mod Zc, cl): the unwrapped candidate is tzb + s*GT; when z + s >= Zc the wrapped
@@ -410,6 +459,37 @@ __device__ __forceinline__ void dec_body(
             putAB(ic, nAs, nBs);
             put_row(ic, negs, idxn);
         };
+        // dead extension row (q_ext = +0, so min1 = 0 and every core r is +-0): q_k = APP_k - (+-0)
+        // = APP_k up to the sign of a zero; only the extension message changes:
+        // r_ext = sign(prod q_k) * alpha * max(min |q_k| - beta, 0) (min2 of the row), APP_ext =
+        // 0 + r_ext.  State as the full update leaves it: mA = +-0, mB = r_ext, argmin = the
+        // extension edge (last), its sign bit 0.
+        auto dead_row = [&](auto ic, auto& gshift) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            T mn = FT<T>::inf();
+            uint32_t sx = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    const int rbk = (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)gshift(e0 + k) * GT);
+                    const T a = at(j * CS * TS + rbk);
+                    mn = fmin(mn, fabs(a));
+                    sx ^= FT<T>::sbits(a);
+                }
+            });
+            T x2 = mn;
+            if constexpr (OFS) {
+                x2 = mn - beta;
+                x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const T nBs = FT<T>::xsign(alpha * x2, sx);
+            hdx |= (uint64_t)(nBs < T(0)) << (i - 4);
+            putAB(ic, T(0), nBs);
+            put_row(ic, 0u, (uint32_t)(d - 1));
+        };
         // the next row group's packed shift words are loaded (scalar, wave-uniform) before the
         // barrier that precedes the group, so their latency hides behind it
         constexpr int NPW = max_group_nw<BG>();
@@ -440,20 +520,35 @@ __device__ __forceinline__ void dec_body(
             uint32_t csw[NPW];
 #pragma unroll
             for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
-            if constexpr (g + 1 < kGroups<BG>.n) prefetch_xl(std::integral_constant<int, g + 1>{});
+            if constexpr (g + 1 < kGroups<BG>.n) {
+                if (!gdead(std::integral_constant<int, g + 1>{}))   // dead groups load nothing
+                    prefetch_xl(std::integral_constant<int, g + 1>{});
+            }
             auto gshift = [&](int e) -> int {   // e compile-time after unrolling
                 const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
                 return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
             };
+            const bool dead = gdead(gc);
             if (active) {
-                sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
-                    layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));
-                });
+                if constexpr (DEAD && group_xmask<BG>(g) != 0) {
+                    if (dead)
+                        sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) { dead_row(ic, gshift); });
+                }
+                if (!dead) {
+                    sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
+                        layered_row(ic, gshift, i >= 4 ? xlb[g & 1][i >= 4 ? i - r0 : 0] : T(0));
+                    });
+                }
             }
             if constexpr (g + 1 < kGroups<BG>.n) prefetch(std::integral_constant<int, g + 1>{});
-            lds_barrier();
+            // dead rows only read the APPs: two dead groups in a row need no barrier between them
+            if constexpr (g + 1 < kGroups<BG>.n) {
+                if (!(dead && gdead(std::integral_constant<int, g + 1>{}))) lds_barrier();
+            } else {
+                lds_barrier();
+            }
         });
 
         {
@@ -554,15 +649,15 @@ __device__ __forceinline__ void dec_body(
     llr, ck, status, iters, B, Zc_u, zi_u, G_u, ldl, ldc, L, alpha, beta, pc, work, cbs
 
 // layered float32: 768 threads = 12 waves = 3 per SIMD (<= 168 VGPRs), G = floor(768/Zc) CBs
-template <int BG, typename T, bool LAYERED, bool OFS>
+template <int BG, typename T, bool LAYERED, bool OFS, bool DEAD = false>
 __global__ __launch_bounds__(kDecThreadsL) __attribute__((amdgpu_waves_per_eu(3))) void
 ldpc_dec_kernel_l(LDPC5G_DEC_PARAMS) {
-    dec_body<BG, T, LAYERED, OFS>(LDPC5G_DEC_ARGS);
+    dec_body<BG, T, LAYERED, OFS, DEAD>(LDPC5G_DEC_ARGS);
 }
-template <int BG, typename T, bool LAYERED, bool OFS = true>
+template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false>
 constexpr auto dec_kernel() {
     static_assert(LAYERED, "the flooding kernels are in ldpc5g_dec_flood.h");
-    return ldpc_dec_kernel_l<BG, T, LAYERED, OFS>;
+    return ldpc_dec_kernel_l<BG, T, LAYERED, OFS, DEAD>;
 }
 
 template <int BG, typename T, bool LAYERED>
@@ -571,18 +666,18 @@ size_t dec_lds_bytes() {
     return dec_lds_bytes_t<BG, T, LAYERED>();
 }
 
-template <int BG, typename T, bool LAYERED>
+template <int BG, typename T, bool LAYERED, bool DEAD = false>
 int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                  int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
-    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD>() : dec_kernel<BG, T, LAYERED, false, DEAD>();
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
     // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
     const int G = std::min(dec_G(Zc, LAYERED), B);
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     const int threads = ((G * Zc + 63) / 64) * 64;
     const int grid = (B + G - 1) / G;
-    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true>()>(lds)
-                             : set_lds_once<dec_kernel<BG, T, LAYERED, false>()>(lds))
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD>()>(lds))
         return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, llr, ck, status, iters, B, Zc, zi,
                        G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
@@ -590,14 +685,14 @@ int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int 
     return check_hip(hipGetLastError(), "ldpc_dec_kernel launch");
 }
 
-template <int BG, typename T, bool LAYERED>
+template <int BG, typename T, bool LAYERED, bool DEAD = false>
 int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
                        const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                        int pc, hipStream_t st) {
-    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true>() : dec_kernel<BG, T, LAYERED, false>();
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD>() : dec_kernel<BG, T, LAYERED, false, DEAD>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
-    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true>()>(lds)
-                             : set_lds_once<dec_kernel<BG, T, LAYERED, false>()>(lds))
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD>()>(lds))
         return rc;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(dec_cs<LAYERED>()), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);

@@ -1,0 +1,34 @@
+// ldpc5g_dec_dead.hip — the flooding decoder's dead-extension-row variants (DEAD = true, float64
+// and float32, batch and mixed work lists), selected by LDPC5G_RATE_MATCHED.
+// Own translation unit: compiles in parallel with the plain instantiations (ldpc5g_dec.hip).
+#include "ldpc5g_dec_flood.h"
+
+namespace ldpc5g_impl {
+
+int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
+                      int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
+                      double alpha, double beta, int pc, hipStream_t st) {
+    if (dtype == LDPC5G_F64) {
+        const double* p = (const double*)llr;
+        return bgn == 1 ? launch_flood_t<1, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                        : launch_flood_t<2, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    }
+    const float* p = (const float*)llr;
+    return bgn == 1 ? launch_flood_t<1, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                    : launch_flood_t<2, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+}
+
+int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
+                            int32_t* iters, int nwg, const DecWork* work, const CbRef* cbs, int L,
+                            double alpha, double beta, int pc, hipStream_t st) {
+    if (dtype == LDPC5G_F64) {
+        const double* p = (const double*)llr;
+        return bgn == 1 ? launch_flood_mixed_t<1, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                        : launch_flood_mixed_t<2, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    }
+    const float* p = (const float*)llr;
+    return bgn == 1 ? launch_flood_mixed_t<1, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
+                    : launch_flood_mixed_t<2, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+}
+
+}  // namespace ldpc5g_impl

@@ -116,6 +116,21 @@ struct FloodPlan {
 template <int BG, typename T, int NP, int CS>
 constexpr FloodPlan<BG, T, NP, CS> kFloodPlan{};
 
+// every core column's first row is one of rows 0..3 (which have no extension column): a dead
+// extension row never initialises a column sum in phase B, so skipping its adds is exact
+template <int BG>
+constexpr bool first_rows_core() {
+    for (int j = 0; j < BGT<BG>::KC; ++j) {
+        int f = -1;
+        for (int i = 0; i < BGT<BG>::MB && f < 0; ++i)
+            for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i + 1]; ++e)
+                if (BGT<BG>::COL[e] == j) f = i;
+        if (f < 0 || f >= 4) return false;
+    }
+    return true;
+}
+static_assert(first_rows_core<1>() && first_rows_core<2>(), "dead-row skipping needs core first rows");
+
 template <int BG, typename T, int NP, int CS>
 constexpr size_t flood_lds_bytes_t() {
     return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T, NP, CS>.nls * CS * (2 * sizeof(T) + 4) +
@@ -149,7 +164,7 @@ __device__ __forceinline__ void two_min(double& m1, double& m2, double a) {
     m1 = fmin(m1, a);
 }
 
-template <int BG, typename T, bool OFS, int NP, int CS>
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD>
 __device__ __forceinline__ void flood_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -221,6 +236,11 @@ __device__ __forceinline__ void flood_body(
     auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
     auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
     auto llrx = [&](int i) -> T { return lrow[(KB + i - pc) * Zc + zv]; };   // ext column of row i
+    auto per_half_init = [&](auto&& f) {
+        sfor<0, NP>([&](auto pc_) {
+            if (h == decltype(pc_)::value) f(pc_);
+        });
+    };
 
     // row state: (mA, mB) magnitudes, the signs of r_k (edge 0 in bit d-1) and the argmin edge;
     // VGPR rows of degree <= 12 keep signs | argmin << 12 in one 16-bit field of a shared word
@@ -271,8 +291,18 @@ __device__ __forceinline__ void flood_body(
     };
 
     // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS row state 0; wrap table
-    if (valid)
+    uint64_t nzx = 0;   // extension columns of this half's rows whose LLR is not +0.0 at this z
+    if (valid) {
         for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+        if constexpr (DEAD)
+            per_half_init([&](auto hc) {
+                sfor<4, MB>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
+                        nzx |= (uint64_t)(FT<T>::bits(llrx(i)) != 0) << (i - 4);
+                });
+            });
+    }
     for (int w = t; w < NLS * CS; w += (int)blockDim.x) {
         V2<T> v;
         v.x = T(0), v.y = T(0);
@@ -281,9 +311,36 @@ __device__ __forceinline__ void flood_body(
     }
     if (s == 0 && h == 0)
         for (int c = 0; c < G; ++c) flagA[c] = 0;
+    uint32_t* livew = (uint32_t*)(anyf + 2);   // workgroup OR of nzx (2 words)
     if (t == 0) *anyf = 0;
+    if constexpr (DEAD)
+        if (t == 0) livew[0] = 0u, livew[1] = 0u;
     bool active = valid;
     lds_barrier();
+    // Dead extension rows (LLR +0.0 in every slot of the workgroup: untransmitted parity at high
+    // code rates): q_ext = (0 + r) - r = +0, so every core message of the row is +-0 and its phase-B
+    // adds change no column sum (their first rows are rows 0..3); only r_ext and the row's syndrome
+    // bit matter.  rowA_dead computes exactly those; dead rows add nothing in phase B, and a group
+    // of dead rows needs no barrier.  Bit-identical to running them (flooding has no ordering
+    // between rows in phase A).
+    uint64_t live_x = ~0ull;
+    if constexpr (DEAD) {
+        if (nzx & 0xffffffffu) atomicOr(&livew[0], (uint32_t)nzx);
+        if (nzx >> 32) atomicOr(&livew[1], (uint32_t)(nzx >> 32));
+        lds_barrier();
+        live_x = ((uint64_t)__builtin_amdgcn_readfirstlane(livew[1]) << 32) |
+                 (uint64_t)__builtin_amdgcn_readfirstlane(livew[0]);
+    }
+    auto rdead = [&](auto ic) -> bool {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (!DEAD || i < 4) return false;
+        else return ((live_x >> (i - 4)) & 1u) == 0;
+    };
+    auto gdead = [&](auto gc) -> bool {
+        constexpr uint64_t m = group_xmask<BG>(decltype(gc)::value);
+        if constexpr (!DEAD || m == 0) return false;
+        else return (live_x & m) == 0;
+    };
 
     // byte offset (without column base) of entry ((z + sft) mod Zc, cl): the unwrapped candidate,
     // or the wrapped one when it is valid (smaller as unsigned).  Arithmetic, not the layered
@@ -377,11 +434,56 @@ __device__ __forceinline__ void flood_body(
             const uint32_t flip = (uint32_t)((int32_t)sx >> 31) & ((1u << d) - 1u);
             put_state(ic, alpha * x1, alpha * x2, negs ^ flip, idx);
         };
+        // dead extension row: LQ_ext = 0 + r_old_ext (its syndrome bit), q_core = LQ - (+-0);
+        // new state as the full update leaves it up to zero signs: nA = 0, nB = alpha * max(
+        // min |q_core| - beta, 0), argmin = the extension edge, whose sign bit is the row sign
+        auto rowA_dead = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            T mA, mB;
+            uint32_t u, idxo;
+            get_state(ic, mA, mB, u, idxo);
+            const T rext = xsign_v(pick(idxo == (uint32_t)(d - 1), mB, mA), u << (d - 1), mv);
+            if constexpr (kXPre > 0) {   // keep the half's ext-LLR ring moving (row p + XP's load)
+                constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
+                xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+            }
+            const T ax = T(0) + rext;
+            hdx |= (uint64_t)(ax < T(0)) << (i - 4);
+            bool par = ax < T(0);
+            T mn = FT<T>::inf();
+            uint32_t sx = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    const T a = at(j * CS * TS + rot(sh(e0 + k)));
+                    par ^= a < T(0);
+                    mn = fmin(mn, fabs(a));
+                    sx ^= FT<T>::sbits(a);
+                }
+            });
+            fail |= par;
+            T x2 = mn;
+            if constexpr (OFS) {
+                x2 = mn - beta;
+                x2 = x2 > T(0) ? x2 : T(0);
+            }
+            put_state(ic, T(0), alpha * x2, sx >> 31, (uint32_t)(d - 1));
+        };
         if (active) {
             per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
             sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
                 constexpr int i = decltype(ic)::value;
-                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) rowA(ic);
+                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
+                    if constexpr (DEAD && i >= 4) {
+                        if (rdead(ic)) rowA_dead(ic);
+                        else rowA(ic);
+                    } else {
+                        rowA(ic);
+                    }
+                }
             });
             if (fail) flagA[cl] = 1;
         }
@@ -476,10 +578,12 @@ __device__ __forceinline__ void flood_body(
                 const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
                 return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
             };
-            if (active) {
+            const bool gd = gdead(gc);   // a dead group adds nothing: no barrier either
+            if (active && !gd) {
                 per_half([&](auto hc) {
                     sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
                         constexpr int i = decltype(ic)::value;
+                        if (rdead(ic)) return;   // +-0 adds (a partly dead group)
                         if constexpr (i < NLS) {   // LDS state: both halves, alternate edges
                             rowB(ic, hc, gshift, cA, cB, cu, cidx);
                         } else if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
@@ -491,7 +595,7 @@ __device__ __forceinline__ void flood_body(
                     });
                 });
             }
-            lds_barrier();
+            if (!gd) lds_barrier();
         });
         // ---- LQ = LLRin + sum (:126) for the own entries
         if (active)
@@ -561,14 +665,14 @@ __device__ __forceinline__ void flood_body(
 
 // NP parts x CS slots: 768 threads (3 waves per SIMD) for batches, 1024 (4 per SIMD) for the
 // 16-part configuration of small launches
-template <int BG, typename T, bool OFS, int NP, int CS>
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
 __global__ __launch_bounds__(NP * CS) __attribute__((amdgpu_waves_per_eu(NP * CS / 256))) void
 ldpc_flood_kernel(LDPC5G_DEC_PARAMS) {
-    flood_body<BG, T, OFS, NP, CS>(LDPC5G_DEC_ARGS);
+    flood_body<BG, T, OFS, NP, CS, DEAD>(LDPC5G_DEC_ARGS);
 }
 
-template <int BG, typename T, bool OFS, int NP, int CS>
-constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS>; }
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
+constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS, DEAD>; }
 
 template <int BG, typename T, int NP, int CS>
 size_t flood_lds_bytes() {
@@ -576,23 +680,23 @@ size_t flood_lds_bytes() {
     return flood_lds_bytes_t<BG, T, NP, CS>();
 }
 
-template <int BG, typename T, int NP, int CS>
+template <int BG, typename T, int NP, int CS, bool DEAD = false>
 int set_flood_lds(bool ofs) {
     const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
-    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS>()>(lds)
-               : set_lds_once<flood_kernel<BG, T, false, NP, CS>()>(lds);
+    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS, DEAD>()>(lds)
+               : set_lds_once<flood_kernel<BG, T, false, NP, CS, DEAD>()>(lds);
 }
 
 // G codeblocks per workgroup (G * Zc <= CS); NP parts of H = G*Zc rounded up to a wave
-template <int BG, typename T, int NP, int CS>
+template <int BG, typename T, int NP, int CS, bool DEAD = false>
 int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                      int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
                      hipStream_t st) {
     const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS> : ldpc_flood_kernel<BG, T, false, NP, CS>;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS, DEAD> : ldpc_flood_kernel<BG, T, false, NP, CS, DEAD>;
     const int H = ((G * Zc + 63) / 64) * 64;
     if (G < 1 || H > CS) return fail(LDPC5G_ESIZE, "flooding launch: %d codeblocks of Zc=%d per workgroup", G, Zc);
-    if (int rc = set_flood_lds<BG, T, NP, CS>(ofs)) return rc;
+    if (int rc = set_flood_lds<BG, T, NP, CS, DEAD>(ofs)) return rc;
     const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
     hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(NP * H), lds, st, llr, ck, status, iters, B, Zc,
                        zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
@@ -603,23 +707,23 @@ int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
 constexpr int kFloodNP = 2, kFloodCS = kDecThreads;   // batch configuration: 2 x 384 slots
 constexpr int kFloodSmallNP = 16, kFloodSmallCS = 64;  // small launches: 16 x 64 slots
 
-template <int BG, typename T>
+template <int BG, typename T, bool DEAD = false>
 int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                    int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks
     const int G = std::min(dec_G(Zc, false), B);
-    return launch_flood_cfg<BG, T, kFloodNP, kFloodCS>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
-                                                       alpha, beta, pc, st);
+    return launch_flood_cfg<BG, T, kFloodNP, kFloodCS, DEAD>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
+                                                             alpha, beta, pc, st);
 }
 
-template <int BG, typename T>
+template <int BG, typename T, bool DEAD = false>
 int launch_flood_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
                          const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                          int pc, hipStream_t st) {
     const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS>
-                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS>;
-    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS>(ofs)) return rc;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS, DEAD>
+                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS, DEAD>;
+    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS, DEAD>(ofs)) return rc;
     const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodNP * kFloodCS), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);

@@ -763,7 +763,7 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
     if (T == 0) return LDPC5G_OK;
     const int Nf = (cfg->bgn == 1 ? 68 : 52) * cfg->Zc;
     if (int rc = ldpc5g_decode_ms(llr_dn, dn_dtype, ck, status, iters, T * cfg->C, cfg->bgn, cfg->Zc, L,
-                                  alpha, beta, schedule, 0, cfg->N, Nf, stream))
+                                  alpha, beta, schedule, LDPC5G_RATE_MATCHED, cfg->N, Nf, stream))
         return rc;
     return ldpc5g_sch_tb_check(ck, Nf, cfg, T, tbblk, ldb, cb_crc_ok, tb_rem, tb_ok, stream);
 }
@@ -848,7 +848,7 @@ int ldpc5g_sch_decode_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
         desc[r].llr_off = G.dn_off + (int64_t)c * G.s.N, desc[r].ck_off = G.dck_off + (int64_t)c * G.dck_ld;
     }
     if (int rc = ldpc5g_decode_ms_mixed(desc.data(), rows, llr_dn, dn_dtype, ck, status, iters, L, alpha, beta,
-                                        schedule, 0, stream))
+                                        schedule, LDPC5G_RATE_MATCHED, stream))
         return rc;
     if (int rc = check_hip(hipMemsetAsync(tb_rem, 0, (size_t)T * 4, st), "hipMemsetAsync")) return rc;
     hipLaunchKernelGGL(tb_check_kernel, dim3(rows), dim3(kCrcNT), 0, st, (const int8_t*)ck, (int64_t)0, s0,

@@ -37,11 +37,15 @@ def _check_algo(algo):
 
 
 def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
-                         schedule="flooding", full=False, out=None):
+                         schedule="flooding", full=False, out=None, rate_matched=False):
     """Decode B codeblocks of one (bgn, Zc).
 
     LLR: (B, N) float64 or float32 — numpy (copied to the GPU and back) or a GPU torch tensor
          (stays on the device).  N = 66Zc / 50Zc, or the full 68Zc / 52Zc when full=True.
+    rate_matched: the rows come from rate recovery, so parity columns that were never transmitted
+         hold +0.0 (LDPC5G_RATE_MATCHED): the min-sum kernels detect rows whose extension column
+         is +0.0 in every codeblock of a workgroup and skip their null updates — same results,
+         much less work at high code rates.
     Returns (ck (B, Nf) int8, status (B,) bool, iters (B,) int32) of the input's kind; for
     device tensors status is uint8 and nothing is synchronised."""
     assert bgn in [1, 2]
@@ -77,7 +81,7 @@ def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
             and st.is_contiguous() and it.is_contiguous(), "out[1]/out[2] must be uint8/int32 (>= B,)"
         assert ck.device == x.device and st.device == x.device and it.device == x.device, \
             "outputs must live on the LLR tensor's device"
-    flags = _lib.LLR_FULL if full else 0
+    flags = (_lib.LLR_FULL if full else 0) | (_lib.RATE_MATCHED if rate_matched else 0)
     lib = _lib.lib()
     with t.cuda.device(x.device):
         stream = _lib.stream_ptr(x.device)
@@ -118,10 +122,15 @@ def _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, full):
                 t.empty((Nf + 8,), dtype=t.uint8, device=dev),
                 t.empty((Nf + 8,), dtype=t.uint8, pin_memory=True))
     hin, din, drec, hrec = _lib.staging(("dec1", dev, n_in, Nf), make)
-    hin.numpy()[0] = np.asarray(LLRin, np.float64).reshape(-1)
+    x = np.asarray(LLRin, np.float64).reshape(-1)
+    hin.numpy()[0] = x
     din.copy_(hin, non_blocking=True)
     out = (drec[:Nf].view(t.int8).view(1, Nf), drec[Nf:Nf + 1], drec[Nf + 4:Nf + 8].view(t.int32))
-    nr_decode_ldpc_batch(din, Zc, bgn, L, algo, alpha, beta, "flooding", full=full, out=out)
+    # a last parity column of exact +0.0 (untransmitted after rate recovery, e.g. DLSCHDecode's
+    # rows at high code rates) enables dead-row skipping: same results, less work
+    rm = algo == "min-sum" and not x[-Zc:].view(np.int64).any()
+    nr_decode_ldpc_batch(din, Zc, bgn, L, algo, alpha, beta, "flooding", full=full, out=out,
+                         rate_matched=rm)
     hrec.copy_(drec, non_blocking=True)
     t.cuda.current_stream().synchronize()
     h = hrec.numpy()

@@ -7,8 +7,10 @@ from . import _lib
 from .ldpc_info import code_dims, find_iLS
 
 
-def decode_mixed(items, L, alpha=1.0, beta=0.0, schedule="flooding"):
+def decode_mixed(items, L, alpha=1.0, beta=0.0, schedule="flooding", rate_matched=False):
     """items: list of (bgn, Zc, llr[N]) with float32 (or all float64) LLR rows.
+    rate_matched: the rows come from rate recovery (LDPC5G_RATE_MATCHED: untransmitted extension
+    columns +0.0 are detected and their null row updates skipped; same results).
     Returns (list of ck int8[Nf] arrays, status bool[B], iters int32[B]) in item order."""
     t = _lib.require_gpu()
     assert schedule in ("flooding", "layered")
@@ -36,8 +38,8 @@ def decode_mixed(items, L, alpha=1.0, beta=0.0, schedule="flooding"):
         _lib.check(_lib.lib().ldpc5g_decode_ms_mixed(
             desc, B, _lib.ptr(x), _lib.F64 if f64 else _lib.F32, _lib.ptr(ck), _lib.ptr(st),
             _lib.ptr(it), int(L), float(alpha), float(beta),
-            _lib.LAYERED if schedule == "layered" else _lib.FLOODING, 0,
-            _lib.stream_ptr(x.device)))
+            _lib.LAYERED if schedule == "layered" else _lib.FLOODING,
+            _lib.RATE_MATCHED if rate_matched else 0, _lib.stream_ptr(x.device)))
     ckh = ck.cpu().numpy()
     return ([ckh[c:c + n].copy() for _, c, n in rows], st.cpu().numpy()[:B].astype(bool),
             it.cpu().numpy()[:B])
@@ -92,15 +94,16 @@ class MixedBatch:
             p = self._plans[schedule] = (host, dev)
         return p
 
-    def decode(self, L, alpha=1.0, beta=0.0, schedule="layered"):
+    def decode(self, L, alpha=1.0, beta=0.0, schedule="layered", rate_matched=False):
         """<= 2 kernel launches on the current stream, asynchronous (no host synchronisation);
-        returns the device buffers (ck flat, status (B,), iters (B,))."""
+        returns the device buffers (ck flat, status (B,), iters (B,)).  rate_matched: see
+        decode_mixed."""
         t = _lib.torch()
         host, dev = self._plan(schedule)
         with t.cuda.device(self.llr.device):
             _lib.check(_lib.lib().ldpc5g_decode_ms_mixed_plan(
                 _lib.ptr(dev), _lib.ptr(host), _lib.ptr(self.llr), _lib.F32, _lib.ptr(self.ck),
                 _lib.ptr(self.status), _lib.ptr(self.iters), int(L), float(alpha), float(beta),
-                _lib.LAYERED if schedule == "layered" else _lib.FLOODING, 0,
-                _lib.stream_ptr(self.llr.device)))
+                _lib.LAYERED if schedule == "layered" else _lib.FLOODING,
+                _lib.RATE_MATCHED if rate_matched else 0, _lib.stream_ptr(self.llr.device)))
         return self.ck, self.status[:self.B], self.iters[:self.B]

@@ -211,7 +211,7 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
         from .nr_ldpc_decode import nr_decode_ldpc_batch
         llr_dn = sch_raterecover_batch(llr, cfg, harq_in, dn_dtype, ws)
         nr_decode_ldpc_batch(llr_dn, cfg.Zc, cfg.bgn, L, algo, alpha, beta, "flooding",
-                             out=(ws.dec_ck, ws.status, ws.iters))
+                             out=(ws.dec_ck, ws.status, ws.iters), rate_matched=True)
         sch_tb_check_batch(ws.dec_ck, cfg, T, ws)
     return SchDecodeResult(ws.tb_ok, ws.tbblk, llr_dn, ws.dec_ck, ws.status, ws.iters, ws.cb_ok,
                            ws.tb_rem)

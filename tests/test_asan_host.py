@@ -15,7 +15,7 @@ from python_5gtoolbox_amd import build
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(2400)   # a stale sanitizer build recompiles changed TUs first
 def test_capi_host_code_under_asan_ubsan():
     lib = build.build_asan()
     rt = build.asan_runtime()

@@ -48,7 +48,7 @@ def test_bit_flipping_toy_kat():
     H = np.array([[1, 1, 0, 1, 0, 0], [0, 1, 1, 0, 1, 0], [1, 0, 0, 0, 1, 1], [0, 0, 1, 1, 0, 1]])
     cw = [x for x in (np.array([(v >> k) & 1 for k in range(6)]) for v in range(64))
           if not ((H @ x) % 2).any()]
-    assert len(cw) == 4
+    assert len(cw) == 8   # rank 3 over GF(2)
     rng = np.random.default_rng(0)
     for dn in cw:
         fn = 1 - 2 * dn + rng.normal(0, 10 ** (-255 / 20), 6)

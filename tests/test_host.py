@@ -40,6 +40,7 @@ def test_header_constants_match_binding():
     assert int(consts["LDPC5G_FLOODING"]) == _lib.FLOODING
     assert int(consts["LDPC5G_LAYERED"]) == _lib.LAYERED
     assert int(consts["LDPC5G_LLR_FULL"]) == _lib.LLR_FULL
+    assert int(consts["LDPC5G_RATE_MATCHED"]) == _lib.RATE_MATCHED
     assert (int(consts["LDPC5G_ALGO_MS"]), int(consts["LDPC5G_ALGO_BP"]),
             int(consts["LDPC5G_ALGO_BF"])) == (_lib.ALGO_MS, _lib.ALGO_BP, _lib.ALGO_BF)
     assert int(consts["LDPC5G_EBGN"]) == _lib.EBGN and int(consts["LDPC5G_EZC"]) == _lib.EZC
