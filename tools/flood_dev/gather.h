@@ -1,0 +1,933 @@
+// ldpc5g_dec_flood.h — flooding min-sum decoder (py5gphy/ldpc/nr_ldpc_decode.py:51-143 with
+// _min_sum_process :178-227), float64 (bit-identical to the reference) and float32.
+//
+// One iteration of the reference computes every check-to-variable message Lr from Lq = LQ_old - Lr_old
+// (:117-123), then LQ_new = LLRin + Lr.sum(axis=0) (:126), a row-ascending sum per column.  The
+// kernel splits it the same way:
+//   phase A  every base row reads LQ_old (LDS, read-only in this phase, no barrier between rows),
+//            forms q = LQ_old - r_old edge by edge and keeps only the new compressed row state
+//            (nA = alpha*max(min1-beta,0), nB = ... min2, per-edge signs, argmin);  the syndrome
+//            of the hard decisions of LQ_old (:107-114) falls out of the same reads;
+//   phase B  the messages r are rebuilt from the new state and summed into the SAME LDS array
+//            (LQ_old is dead now) in row-ascending order, one barrier per group of column-disjoint
+//            rows; the first row of each column writes 0 + r instead of adding;
+//   then     LQ = LLR + sum for the thread's own entries.
+// So one f64 array of the Kb+4 core columns (80 KB at Zc = 384) is the whole LDS image of LQ, and
+// the remaining LDS holds the state of the first rows.  Every thread slot (z, codeblock) has two
+// threads, one per half of the 768-thread workgroup (6 waves each, 3 waves per SIMD): the base rows
+// are split between the halves (phase-A edge counts balanced, the rows of a multi-row group on
+// different halves so phase B stays balanced), so each thread holds the state of ~half the rows
+// in VGPRs.  Rows whose state lives in LDS are summed by both halves (alternate edges) in phase B.
+#pragma once
+#include "ldpc5g_dec_body.h"
+
+namespace ldpc5g_impl {
+namespace {
+
+constexpr size_t kLdsPerCU = 160 * 1024;
+#ifndef LDPC5G_FLOOD_XPRE
+#define LDPC5G_FLOOD_XPRE 4
+#endif
+// extension-column LLRs are loaded this many ext rows ahead of their use in phase A
+constexpr int kXPre = LDPC5G_FLOOD_XPRE;
+#ifndef LDPC5G_GATHER_ILP
+#define LDPC5G_GATHER_ILP 4
+#endif
+// gather phase B: edges per scheduling region (their LDS reads may be in flight together)
+constexpr int kGatherILP = LDPC5G_GATHER_ILP;
+
+// Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
+// state lives, and the packing of its sign word.  NP = 2, CS = 384 for batches; NP = 16, CS = 64 for
+// the small launches of the per-codeblock drop-ins (16 waves share one codeblock's rows).
+template <int BG, typename T, int NP, int CS>
+struct FloodPlan {
+    int nls = 0;          // rows 0..nls-1 keep their state in LDS
+    int owner[64] = {};   // part that runs phase A of row i (and phase B of a VGPR row)
+    int slot[64] = {};    // VGPR state slot of row i in its owner part (-1: LDS row)
+    int nslot = 0;
+    int pw[64] = {};      // VGPR sign word of row i: rows of degree <= 12 share a word (16-bit fields)
+    int ph[64] = {};      // 0: whole word (negs | idx << 24), 1: low field, 2: high field (negs | idx << 12)
+    int npw = 0;
+    int first_row[32] = {};   // lowest base row of core column j (writes 0 + r in phase B)
+    int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner part's ext rows
+    int xlist[NP][64] = {};   // ext rows of each part, ascending
+    int nx[NP] = {};
+    // Gather phase B (the 2-part batch configuration): core column j is summed by part cown[j]
+    // (index cpos[j] among its ncol columns; parts balanced by column degree) in VGPRs.  The row
+    // states are read from LDS in row chunks: chunk 0 = the LDS rows, chunk c >= 1 = rows
+    // [cr0[c], cr0[c+1]) written by their owners into row slots (slot_off: the (mA, mB) array, the
+    // sign/argmin words follow at + CS * 2 * sizeof(T)), double-buffered by chunk parity in the
+    // LQ array (dead during phase B) and the LDS left after the flags.
+    static constexpr bool GATHER = NP == 2;
+    int cown[32] = {};
+    int cpos[32] = {};
+    int ncol[NP] = {};
+    int clist[NP][32] = {};
+    int rh = 0, nchunk = 0;
+    int cr0[66] = {};
+    int slot_off[64] = {};
+    int lds_end = 0;
+    static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
+    constexpr FloodPlan() {
+        using P = BGT<BG>;
+        const auto& G = kGroups<BG>;
+        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4;
+        const int fit = (int)((kLdsPerCU - fixed) / (CS * (2 * sizeof(T) + 4)));
+        int lead = 0;   // leading single-row groups: their phase B is split only if in LDS
+        while (lead < G.n && G.start[lead + 1] - G.start[lead] == 1 && G.start[lead] == lead) ++lead;
+        nls = fit < lead ? fit : lead;
+        int load[NP] = {};
+        bool done[64] = {};
+        // rows of a multi-row group on different parts (phase B balance), then every other row
+        // by decreasing degree onto the least loaded part (phase A balance)
+        for (int g = 0; g < G.n; ++g) {
+            if (G.start[g + 1] - G.start[g] < 2) continue;
+            int gl[NP] = {};
+            for (;;) {
+                int best = -1;
+                for (int i = G.start[g]; i < G.start[g + 1]; ++i)
+                    if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
+                if (best < 0) break;
+                int h = 0;
+                for (int q = 1; q < NP; ++q)
+                    if (gl[q] < gl[h] || (gl[q] == gl[h] && load[q] < load[h])) h = q;
+                owner[best] = h, gl[h] += deg(best), load[h] += deg(best), done[best] = true;
+            }
+        }
+        for (;;) {
+            int best = -1;
+            for (int i = 0; i < P::MB; ++i)
+                if (!done[i] && (best < 0 || deg(i) > deg(best))) best = i;
+            if (best < 0) break;
+            int h = 0;
+            for (int q = 1; q < NP; ++q)
+                if (load[q] < load[h]) h = q;
+            owner[best] = h, load[h] += deg(best), done[best] = true;
+        }
+        int ns[NP] = {};
+        for (int i = 0; i < P::MB; ++i) slot[i] = i < nls ? -1 : ns[owner[i]]++;
+        for (int q = 0; q < NP; ++q) nslot = nslot > ns[q] ? nslot : ns[q];
+        for (int hh = 0; hh < NP; ++hh) {
+            int n = 0, open = -1;
+            for (int i = nls; i < P::MB; ++i) {
+                if (owner[i] != hh) continue;
+                if (deg(i) > 12) {
+                    pw[i] = n++, ph[i] = 0;
+                } else if (open >= 0) {
+                    pw[i] = open, ph[i] = 2, open = -1;
+                } else {
+                    open = n, pw[i] = n++, ph[i] = 1;
+                }
+            }
+            npw = npw > n ? npw : n;
+        }
+        for (int i = 4; i < P::MB; ++i) {
+            xpos[i] = nx[owner[i]];
+            xlist[owner[i]][nx[owner[i]]++] = i;
+        }
+        for (int j = 0; j < P::KC; ++j) {
+            first_row[j] = -1;
+            for (int i = 0; i < P::MB && first_row[j] < 0; ++i)
+                for (int e = P::RS[i]; e < P::RS[i + 1]; ++e)
+                    if (P::COL[e] == j) first_row[j] = i;
+        }
+        // gather plan: columns by decreasing degree onto the part with fewer summed edges
+        int cdeg[32] = {}, cl[NP] = {};
+        bool cd[32] = {};
+        for (int e = 0; e < P::E; ++e)
+            if (P::COL[e] < P::KC) ++cdeg[P::COL[e]];
+        for (;;) {
+            int best = -1;
+            for (int j = 0; j < P::KC; ++j)
+                if (!cd[j] && (best < 0 || cdeg[j] > cdeg[best])) best = j;
+            if (best < 0) break;
+            int hh = 0;
+            for (int q = 1; q < NP; ++q)
+                if (cl[q] < cl[hh]) hh = q;
+            cown[best] = hh, cl[hh] += cdeg[best], cd[best] = true;
+        }
+        for (int j = 0; j < P::KC; ++j) cpos[j] = ncol[cown[j]], clist[cown[j]][ncol[cown[j]]++] = j;
+        const int ss = CS * (2 * (int)sizeof(T) + 4);   // one row slot
+        const int na = P::KC * CS * (int)sizeof(T) / ss;
+        const int tailb = (int)((fixed + (size_t)nls * CS * (2 * sizeof(T) + 4) + 15) / 16 * 16);
+        const int nt = ((int)kLdsPerCU - tailb) / ss;
+        int nsl = na + nt;
+        nsl = nsl > 64 ? 64 : nsl;
+        rh = nsl / 2;
+        for (int k = 0; k < nsl; ++k) slot_off[k] = k < na ? k * ss : tailb + (k - na) * ss;
+        lds_end = nt > 0 && nsl > na ? tailb + (nsl - na) * ss : 0;
+        cr0[0] = 0, nchunk = 1;
+        for (int r = nls; r < P::MB && rh > 0; r += rh) cr0[nchunk++] = r;
+        cr0[nchunk] = P::MB;
+    }
+};
+template <int BG, typename T, int NP, int CS>
+constexpr FloodPlan<BG, T, NP, CS> kFloodPlan{};
+
+// every core column's first row is one of rows 0..3 (which have no extension column): a dead
+// extension row never initialises a column sum in phase B, so skipping its adds is exact
+template <int BG>
+constexpr bool first_rows_core() {
+    for (int j = 0; j < BGT<BG>::KC; ++j) {
+        int f = -1;
+        for (int i = 0; i < BGT<BG>::MB && f < 0; ++i)
+            for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i + 1]; ++e)
+                if (BGT<BG>::COL[e] == j) f = i;
+        if (f < 0 || f >= 4) return false;
+    }
+    return true;
+}
+static_assert(first_rows_core<1>() && first_rows_core<2>(), "dead-row skipping needs core first rows");
+
+template <int BG, typename T, int NP, int CS>
+constexpr size_t flood_lds_bytes_t() {
+    const size_t base = (size_t)BGT<BG>::KC * CS * sizeof(T) +
+                        (size_t)kFloodPlan<BG, T, NP, CS>.nls * CS * (2 * sizeof(T) + 4) + (2 * kMaxG + 4) * 4;
+    const size_t end = (size_t)kFloodPlan<BG, T, NP, CS>.lds_end;
+    return kFloodPlan<BG, T, NP, CS>.GATHER && end > base ? end : base;
+}
+
+// x with its sign flipped by bit 31 of u (all-VGPR v_bitop3: x ^ (u & mv), mv = 0x80000000)
+__device__ __forceinline__ float xsign_v(float x, uint32_t u, uint32_t mv) {
+    return __uint_as_float(__builtin_amdgcn_bitop3_b32(u, __float_as_uint(x), mv, 0x6c));
+}
+__device__ __forceinline__ double xsign_v(double x, uint32_t u, uint32_t mv) {
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32(u, (uint32_t)__double2hiint(x), mv, 0x6c);
+    return __hiloint2double((int)hi, __double2loint(x));
+}
+template <int BG>
+__device__ __forceinline__ const uint32_t* shift_row(int zi) {
+    if constexpr (BG == 1) return kBG1ShiftMod[zi];
+    else return kBG2ShiftMod[zi];
+}
+// c ? a : b on values (a conditional on two lvalues may become a select of their addresses, which
+// keeps the state arrays out of registers)
+template <typename T>
+__device__ __forceinline__ T pick(bool c, T a, T b) { return c ? a : b; }
+// two-min update with min1 <= min2 (values are selected, never rounded: any form is exact)
+__device__ __forceinline__ void two_min(float& m1, float& m2, float a) {
+    m2 = __builtin_amdgcn_fmed3f(m1, m2, a);
+    m1 = fminf(m1, a);
+}
+__device__ __forceinline__ void two_min(double& m1, double& m2, double a) {
+    m2 = fmin(m2, fmax(m1, a));
+    m1 = fmin(m1, a);
+}
+
+#define FP (kFloodPlan<BG, T, NP, CS>)   // the row plan of this instantiation (inside flood_body)
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD>
+__device__ __forceinline__ void flood_body(
+    const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
+    int L, T alpha, T beta, int pc, const DecWork* __restrict__ work,
+    const CbRef* __restrict__ cbs) {
+    using P = BGT<BG>;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = sizeof(T);
+    constexpr int NLS = kFloodPlan<BG, T, NP, CS>.nls;
+    constexpr int NS = kFloodPlan<BG, T, NP, CS>.nslot > 0 ? kFloodPlan<BG, T, NP, CS>.nslot : 1;
+    constexpr int NPW = kFloodPlan<BG, T, NP, CS>.npw > 0 ? kFloodPlan<BG, T, NP, CS>.npw : 1;
+    constexpr int ST_B = KC * CS * TS;               // LDS rows: (mA, mB) pairs
+    constexpr int PK_B = ST_B + NLS * CS * 2 * TS;   // LDS rows: sign/argmin words
+    constexpr int FLAG_B = PK_B + NLS * CS * 4;
+    constexpr int KH = (KC + NP - 1) / NP;   // own columns [h*KH, (h+1)*KH) are part h's
+    constexpr bool GATHER = FP.GATHER;   // gather phase B: own columns are FP.clist[h]
+    static_assert(!GATHER || (FP.rh > 0 && FP.nchunk >= 2), "gather phase B needs row slots");
+    constexpr int NCM = FP.ncol[0] > FP.ncol[NP - 1] ? FP.ncol[0] : FP.ncol[NP - 1];
+    extern __shared__ __align__(16) unsigned char smem[];
+
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
+    int Zc = Zc_u, zi = zi_u, G = G_u;
+    const int t = threadIdx.x;
+    const int H = (int)blockDim.x / NP;   // slots per part, a multiple of 64 (<= CS)
+    const int h = __builtin_amdgcn_readfirstlane(t / H);
+    const int s = t - h * H;
+    if (work) {
+        DecWork w = work[blockIdx.x];
+        Zc = w.Zc, zi = w.zi, G = w.G;
+    }
+    // slot s = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
+    // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
+    const int z = s / G;
+    const int cbl = s - z * G;
+    bool valid = z < Zc;
+    const T* lrow = llr;
+    int8_t* crow = ck;
+    int out = 0;
+    if (valid) {
+        if (work) {
+            CbRef r = cbs[work[blockIdx.x].first + cbl];
+            lrow = llr + r.llr_off;
+            crow = ck + r.ck_off;
+            out = r.out;
+        } else {
+            const int cb = blockIdx.x * G + cbl;   // slots past the batch keep lrow = llr
+            valid = cb < B;
+            if (valid) {
+                lrow = llr + (int64_t)cb * ldl;
+                crow = ck + (int64_t)cb * ldc;
+                out = cb;
+            }
+        }
+    }
+    const int cl = valid ? cbl : 0;
+    const int so = valid ? s : 0;
+    const int tzb = so * TS;   // byte offset of this slot's own column entry
+    const int zg = valid ? z : 0;   // loads issued without a branch stay in row 0 of CB 0
+    int zv = zg, ziv = zi;
+    int* flagA = (int*)(smem + FLAG_B);
+    int* anyf = flagA + 2 * kMaxG;
+    int epoch = 0;
+    auto block_any = [&](bool p) -> bool {
+        ++epoch;
+        if (p) *anyf = epoch;
+        lds_barrier();
+        return *anyf == epoch;
+    };
+    using lds_T = __attribute__((address_space(3))) T;
+    using lds_V2 = __attribute__((address_space(3))) V2<T>;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
+    auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
+    auto llrx = [&](int i) -> T { return lrow[(KB + i - pc) * Zc + zv]; };   // ext column of row i
+    // channel LLR of core column j (compile-time): 0 for the punctured columns 0, 1 when the rows
+    // start at column 2 (pc = 2); branch-free (a load from row 0, then a select)
+    auto llr_core = [&](int j) -> T {
+        if (j >= 2) return lrow[(j - pc) * Zc + zv];
+        const T v = lrow[(pc > j ? 0 : j) * Zc + zv];
+        return pc > j ? T(0) : v;
+    };
+    auto per_half_init = [&](auto&& f) {
+        sfor<0, NP>([&](auto pc_) {
+            if (h == decltype(pc_)::value) f(pc_);
+        });
+    };
+
+    // row state: (mA, mB) magnitudes, the signs of r_k (edge 0 in bit d-1) and the argmin edge;
+    // VGPR rows of degree <= 12 keep signs | argmin << 12 in one 16-bit field of a shared word
+    T sA[NS], sB[NS];
+    uint32_t sP[NPW];
+#pragma unroll
+    for (int x = 0; x < NS; ++x) sA[x] = T(0), sB[x] = T(0);
+#pragma unroll
+    for (int x = 0; x < NPW; ++x) sP[x] = 0u;
+    // u: bit 31 = sign of r_0 (u << k: of r_k), idx: argmin edge
+    auto get_state = [&](auto ic, T& a, T& b, uint32_t& u, uint32_t& idx) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int d = BGT<BG>::RS[i + 1] - BGT<BG>::RS[i];
+        if constexpr (i < NLS) {
+            const V2<T> v = *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + (i * CS) * 2 * TS + 2 * tzb);
+            a = v.x, b = v.y;
+            // word = signs << (32 - d) | argmin: bit 31 = sign of r_0, the argmin in the low byte
+            // (below the lowest sign bit; u is only ever shifted left by < d, so it never reaches 31)
+            const uint32_t p = *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + (i * CS) * 4 + so * 4);
+            u = p, idx = p & 0xffu;
+            asm volatile("" : "+v"(idx));   // compare idx itself with inline constants k
+        } else {
+            constexpr int x = kFloodPlan<BG, T, NP, CS>.slot[i];
+            constexpr int w = kFloodPlan<BG, T, NP, CS>.pw[i];
+            constexpr int f = kFloodPlan<BG, T, NP, CS>.ph[i];
+            a = sA[x], b = sB[x];
+            const uint32_t p = sP[w];
+            if constexpr (f == 0) u = p << (32 - d), idx = p >> 24;
+            else if constexpr (f == 1) u = p << (32 - d), idx = (p >> 12) & 0xfu;
+            else u = p << (16 - d), idx = p >> 28;
+            asm volatile("" : "+v"(idx));
+        }
+    };
+    auto put_state = [&](auto ic, T a, T b, uint32_t negs, uint32_t idx) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NLS) {
+            V2<T> v;
+            v.x = a, v.y = b;
+            *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + (i * CS) * 2 * TS + 2 * tzb) = v;
+            constexpr int d = BGT<BG>::RS[i + 1] - BGT<BG>::RS[i];
+            *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + (i * CS) * 4 + so * 4) = (negs << (32 - d)) | idx;
+        } else {
+            constexpr int x = kFloodPlan<BG, T, NP, CS>.slot[i];
+            constexpr int w = kFloodPlan<BG, T, NP, CS>.pw[i];
+            constexpr int f = kFloodPlan<BG, T, NP, CS>.ph[i];
+            sA[x] = a, sB[x] = b;
+            if constexpr (f == 0) sP[w] = negs | (idx << 24);
+            else if constexpr (f == 1) sP[w] = (sP[w] & 0xffff0000u) | negs | (idx << 12);
+            else sP[w] = (sP[w] & 0xffffu) | (negs << 16) | (idx << 28);
+        }
+    };
+
+    // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS row state 0; wrap table
+    uint64_t nzx = 0;   // extension columns of this half's rows whose LLR is not +0.0 at this z
+    uint32_t hdo = 0;   // gather: hard decisions (LQ < 0) of the part's own columns, bit x = clist[h][x]
+    if (valid) {
+        if constexpr (GATHER) {
+            per_half_init([&](auto hc) {
+                constexpr int hh = decltype(hc)::value;
+                sfor<0, FP.ncol[hh]>([&](auto xc) {
+                    constexpr int x = decltype(xc)::value, j = FP.clist[hh][x];
+                    const T v = llr_core(j);
+                    own(j) = v;
+                    hdo |= (uint32_t)(v < T(0)) << x;
+                });
+            });
+        } else {
+            for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+        }
+        if constexpr (DEAD)
+            per_half_init([&](auto hc) {
+                sfor<4, MB>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
+                        nzx |= (uint64_t)(FT<T>::bits(llrx(i)) != 0) << (i - 4);
+                });
+            });
+    }
+    for (int w = t; w < NLS * CS; w += (int)blockDim.x) {
+        V2<T> v;
+        v.x = T(0), v.y = T(0);
+        *(lds_V2*)(uintptr_t)(uint32_t)(ST_B + w * 2 * TS) = v;
+        *(lds_u32*)(uintptr_t)(uint32_t)(PK_B + w * 4) = 0u;
+    }
+    if (s == 0 && h == 0)
+        for (int c = 0; c < G; ++c) flagA[c] = 0;
+    uint32_t* livew = (uint32_t*)(anyf + 2);   // workgroup OR of nzx (2 words)
+    if (t == 0) *anyf = 0;
+    if constexpr (DEAD)
+        if (t == 0) livew[0] = 0u, livew[1] = 0u;
+    bool active = valid;
+    lds_barrier();
+    // Dead extension rows (LLR +0.0 in every slot of the workgroup: untransmitted parity at high
+    // code rates): q_ext = (0 + r) - r = +0, so every core message of the row is +-0 and its phase-B
+    // adds change no column sum (their first rows are rows 0..3); only r_ext and the row's syndrome
+    // bit matter.  rowA_dead computes exactly those; dead rows add nothing in phase B, and a group
+    // of dead rows needs no barrier.  Bit-identical to running them (flooding has no ordering
+    // between rows in phase A).
+    uint64_t live_x = ~0ull;
+    if constexpr (DEAD) {
+        if (nzx & 0xffffffffu) atomicOr(&livew[0], (uint32_t)nzx);
+        if (nzx >> 32) atomicOr(&livew[1], (uint32_t)(nzx >> 32));
+        lds_barrier();
+        live_x = ((uint64_t)__builtin_amdgcn_readfirstlane(livew[1]) << 32) |
+                 (uint64_t)__builtin_amdgcn_readfirstlane(livew[0]);
+    }
+    auto rdead = [&](auto ic) -> bool {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (!DEAD || i < 4) return false;
+        else return ((live_x >> (i - 4)) & 1u) == 0;
+    };
+    auto gdead = [&](auto gc) -> bool {
+        constexpr uint64_t m = group_xmask<BG>(decltype(gc)::value);
+        if constexpr (!DEAD || m == 0) return false;
+        else return (live_x & m) == 0;
+    };
+
+    // byte offset (without column base) of entry ((z + sft) mod Zc, cl): the unwrapped candidate,
+    // or the wrapped one when it is valid (smaller as unsigned).  Arithmetic, not the layered
+    // kernel's LDS wrap table: phase B is a chain of dependent LDS round trips per row group, and
+    // a table lookup adds one (measured: 4.85 -> 4.53 ms per 4096 f64 codeblocks without it)
+    const uint32_t GT = (uint32_t)(G * TS), tzbw = (uint32_t)tzb - (uint32_t)(Zc * G * TS);
+    auto rot = [&](int sft) -> int {
+        const uint32_t S = (uint32_t)sft * GT;
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
+    // f(integral_constant<half>): each half's rows form one basic block, so the scheduler can
+    // overlap a row's LDS reads with the previous row's arithmetic
+    auto per_half = [&](auto&& f) {
+        sfor<0, NP>([&](auto pc_) {
+            if (h == decltype(pc_)::value) f(pc_);
+        });
+    };
+    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
+    asm volatile("" : "+v"(mv));
+
+    int it = 0;
+    for (; it < L; ++it) {
+        // zv / ziv opaque per iteration: otherwise LICM hoists the ~300 loop-invariant shift
+        // words and column addresses out of the loop into registers
+        zv = zg;
+        ziv = zi;
+        asm volatile("" : "+v"(zv));
+        asm volatile("" : "+s"(ziv));
+        bool fail = false;
+        uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
+        // shift words of this lifting size: one base pointer (SGPR pair), immediate offsets
+        const uint32_t* __restrict__ swrow = shift_row<BG>(ziv);
+        auto sh = [&](int e) -> int {   // e compile-time after unrolling
+            const uint32_t w = swrow[e >> 1];
+            return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+        };
+
+        // ext LLR ring: slot p % XP holds the LLR of the half's ext row p, loaded XP rows ahead
+        constexpr int XP = kXPre > 0 ? kXPre : 1;
+        T xr[XP];
+        auto xload = [&](auto hc, auto pc_) {
+            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
+            if constexpr (kXPre > 0 && p < kFloodPlan<BG, T, NP, CS>.nx[hh])
+                xr[p % XP] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][p]);
+        };
+        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202)
+        auto rowA = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            T mA, mB;
+            uint32_t u, idxo;   // u: bit 31 = sign of r_k for the edge k being visited
+            get_state(ic, mA, mB, u, idxo);
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t sx = 0, idx = 0, negs = 0;
+            bool par = false;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                const T rold = xsign_v(pick(idxo == (uint32_t)k, mB, mA), u, mv);
+                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
+                T a;
+                if constexpr (j < KC) {
+                    a = at(j * CS * TS + rot(sh(e0 + k)));
+                } else {
+                    constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
+                    if constexpr (kXPre > 0) {
+                        a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
+                        xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+                    } else {
+                        a = llrx(i) + rold;
+                    }
+                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                }
+                par ^= a < T(0);
+                const T q = a - rold;
+                const T aq = fabs(q);
+                idx = aq < min1 ? (uint32_t)k : idx;
+                asm volatile("" : "+v"(idx));   // update in place: a sunk select chain keeps all
+                                                // the compare masks live (scratch spills)
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                two_min(min1, min2, aq);
+                sx ^= FT<T>::sbits(q);
+            });
+            fail |= par;
+            T x1 = min1, x2 = min2;
+            if constexpr (OFS) {
+                x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
+                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const uint32_t flip = (uint32_t)((int32_t)sx >> 31) & ((1u << d) - 1u);
+            put_state(ic, alpha * x1, alpha * x2, negs ^ flip, idx);
+        };
+        // dead extension row: LQ_ext = 0 + r_old_ext (its syndrome bit), q_core = LQ - (+-0);
+        // new state as the full update leaves it up to zero signs: nA = 0, nB = alpha * max(
+        // min |q_core| - beta, 0), argmin = the extension edge, whose sign bit is the row sign
+        auto rowA_dead = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int e0 = P::RS[i];
+            constexpr int d = P::RS[i + 1] - e0;
+            T mA, mB;
+            uint32_t u, idxo;
+            get_state(ic, mA, mB, u, idxo);
+            const T rext = xsign_v(pick(idxo == (uint32_t)(d - 1), mB, mA), u << (d - 1), mv);
+            if constexpr (kXPre > 0) {   // keep the half's ext-LLR ring moving (row p + XP's load)
+                constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
+                xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+            }
+            const T ax = T(0) + rext;
+            hdx |= (uint64_t)(ax < T(0)) << (i - 4);
+            bool par = ax < T(0);
+            T mn = FT<T>::inf();
+            uint32_t sx = 0;
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int j = P::COL[e0 + k];
+                if constexpr (j < KC) {
+                    const T a = at(j * CS * TS + rot(sh(e0 + k)));
+                    par ^= a < T(0);
+                    mn = fmin(mn, fabs(a));
+                    sx ^= FT<T>::sbits(a);
+                }
+            });
+            fail |= par;
+            T x2 = mn;
+            if constexpr (OFS) {
+                x2 = mn - beta;
+                x2 = x2 > T(0) ? x2 : T(0);
+            }
+            put_state(ic, T(0), alpha * x2, sx >> 31, (uint32_t)(d - 1));
+        };
+        if (active) {
+            per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
+            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
+                constexpr int i = decltype(ic)::value;
+                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
+                    if constexpr (DEAD && i >= 4) {
+                        if (rdead(ic)) rowA_dead(ic);
+                        else rowA(ic);
+                    } else {
+                        rowA(ic);
+                    }
+                }
+            });
+            if (fail) flagA[cl] = 1;
+        }
+        if constexpr (GATHER) {
+            lds_barrier();   // phase A done: LQ_old is dead, the LDS rows hold their new state
+            // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
+            if (active && flagA[cl] == 0) {
+                per_half([&](auto hc) {
+                    constexpr int hh = decltype(hc)::value;
+                    sfor<0, FP.ncol[hh]>([&](auto xc) {
+                        constexpr int x = decltype(xc)::value;
+                        crow[FP.clist[hh][x] * Zc + zv] = (int8_t)((hdo >> x) & 1u);
+                    });
+                    sfor<4, MB>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        if constexpr (FP.owner[i] == hh) crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
+                    });
+                });
+                if (z == 0 && h == 0) status[out] = 1, iters[out] = it;
+                active = false;
+            }
+            // ---- phase B, gathered: Lr.sum(axis=0) (:126) by the owner of each column entry, in
+            //      VGPRs, row-ascending (0 + r_first + ...); r of edge (i, j) is rebuilt from row i's
+            //      state at check position (z - V) mod Zc, read from LDS chunk by chunk
+            // (recomputed from an opaque copy per iteration: kept live across phase A they would
+            // push it over the 3-waves-per-SIMD VGPR budget)
+            uint32_t sov = (uint32_t)so;
+            asm volatile("" : "+v"(sov));
+            const uint32_t G4 = (uint32_t)(G * 4), so4 = sov * 4u, so4w = so4 - (uint32_t)(Zc * G * 4);
+            T acc[NCM], lf[NCM];
+#pragma unroll
+            for (int x = 0; x < NCM; ++x) acc[x] = T(0);
+            sfor<0, FP.nchunk>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                if (active)
+                    per_half([&](auto hc) {
+                        constexpr int hh = decltype(hc)::value;
+                        // the core LLRs of the LQ update, loaded during the last chunk (registers)
+                        if constexpr (c + 1 == FP.nchunk)
+                            sfor<0, FP.ncol[hh]>([&](auto xc) {
+                                constexpr int x = decltype(xc)::value, j = FP.clist[hh][x];
+                                lf[x] = llr_core(j);
+                            });
+                        // chunk c + 1's VGPR rows into their slots (buffer (c + 1) & 1)
+                        if constexpr (c + 1 < FP.nchunk)
+                            sfor<FP.cr0[c + 1], FP.cr0[c + 2]>([&](auto ic) {
+                                constexpr int i = decltype(ic)::value;
+                                if constexpr (FP.owner[i] == hh) {
+                                    if (rdead(ic)) return;   // never gathered
+                                    constexpr int so_b = FP.slot_off[((c + 1) & 1) * FP.rh + i - FP.cr0[c + 1]];
+                                    T a, b;
+                                    uint32_t u, x;
+                                    get_state(ic, a, b, u, x);
+                                    V2<T> v;
+                                    v.x = a, v.y = b;
+                                    *(lds_V2*)(uintptr_t)(uint32_t)(so_b + so * 2 * TS) = v;
+                                    *(lds_u32*)(uintptr_t)(uint32_t)(so_b + CS * 2 * TS + so * 4) = (u & 0xffffff00u) | x;
+                                }
+                            });
+                        // chunk c: every edge of a column this part owns
+                        sfor<FP.cr0[c], FP.cr0[c + 1]>([&](auto ic) {
+                            constexpr int i = decltype(ic)::value;
+                            constexpr int e0 = P::RS[i];
+                            constexpr int d = P::RS[i + 1] - e0;
+                            // a dead row sends +-0 to its core columns; acc is never -0 (it starts
+                            // as 0 + r), so skipping those adds is exact
+                            if (rdead(ic)) return;
+                            constexpr int vb = c == 0 ? ST_B + i * CS * 2 * TS
+                                                      : FP.slot_off[(c & 1) * FP.rh + i - FP.cr0[c]];
+                            constexpr int ub = c == 0 ? PK_B + i * CS * 4 : vb + CS * 2 * TS;
+                            sfor<0, d>([&](auto kc) {
+                                constexpr int k = decltype(kc)::value;
+                                constexpr int j = P::COL[e0 + k];
+                                if constexpr (j < KC && FP.cown[j] == hh) {
+                                    const uint32_t S4 = (uint32_t)(Zc - sh(e0 + k)) * G4;
+                                    const uint32_t e4 = min(so4 + S4, so4w + S4);
+                                    // the word first, then only the magnitude it selects
+                                    const uint32_t w = *(lds_u32*)(uintptr_t)(ub + e4);
+                                    const uint32_t va = vb + e4 * (2 * TS / 4) + ((w & 0xffu) == (uint32_t)k ? TS : 0);
+                                    const T r = xsign_v(*(lds_T*)(uintptr_t)va, w << k, mv);
+                                    acc[FP.cpos[j]] = acc[FP.cpos[j]] + r;
+                                    // at most kGatherILP edges' reads in flight: hoisting a whole
+                                    // chunk's LDS reads would spill the row state
+                                    constexpr int n = [] {
+                                        int m = 0;
+                                        for (int ii = FP.cr0[c]; ii <= i; ++ii)
+                                            for (int e = P::RS[ii]; e < (ii < i ? P::RS[ii + 1] : e0 + k); ++e)
+                                                m += P::COL[e] < KC && FP.cown[P::COL[e]] == hh;
+                                        return m;
+                                    }();
+                                    if constexpr (n % kGatherILP == kGatherILP - 1) __builtin_amdgcn_sched_barrier(0);
+                                }
+                            });
+                        });
+                    });
+                lds_barrier();
+            });
+            // ---- LQ = LLRin + sum (:126) for the own entries
+            if (active) {
+                hdo = 0;
+                per_half([&](auto hc) {
+                    constexpr int hh = decltype(hc)::value;
+                    sfor<0, FP.ncol[hh]>([&](auto xc) {
+                        constexpr int x = decltype(xc)::value;
+                        const T v = lf[x] + acc[x];
+                        own(FP.clist[hh][x]) = v;
+                        hdo |= (uint32_t)(v < T(0)) << x;
+                    });
+                });
+            }
+        } else {
+        // phase B's shift words are loaded one row group ahead (scalar loads issued before the
+            // barrier that precedes the group, so their latency hides behind it)
+            constexpr int NPW = max_group_nw<BG>();
+            uint32_t nsw[NPW];
+            auto prefetch = [&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                sfor<0, group_nw<BG>(g)>([&](auto wc) {
+                    constexpr int w = decltype(wc)::value;
+                    nsw[w] = swrow[group_w0<BG>(g) + w];
+                });
+            };
+            // the LDS-held state of the next group's row (rows < NLS are single-row groups) is read
+            // one group ahead as well: phase A wrote it before the barrier that precedes phase B
+            T qA = T(0), qB = T(0);
+            uint32_t qu = 0, qidx = 0;
+            auto prefetch_state = [&](auto gc) {
+                constexpr int r = kGroups<BG>.start[decltype(gc)::value];
+                if constexpr (r < NLS) get_state(std::integral_constant<int, r>{}, qA, qB, qu, qidx);
+            };
+            prefetch(std::integral_constant<int, 0>{});
+            lds_barrier();
+            prefetch_state(std::integral_constant<int, 0>{});
+            // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
+            if (active && flagA[cl] == 0) {
+                for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
+                per_half([&](auto hc) {
+                    sfor<4, MB>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
+                            crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
+                    });
+                });
+                if (z == 0 && h == 0) status[out] = 1, iters[out] = it;
+                active = false;
+            }
+    
+            // ---- phase B: Lr.sum(axis=0) in row order into the LQ array (:126)
+            auto rowB = [&](auto ic, auto splitc, auto& gshift, T nA, T nB, uint32_t u, uint32_t idxn) {
+                constexpr int i = decltype(ic)::value;
+                constexpr int e0 = P::RS[i];
+                constexpr int d = P::RS[i + 1] - e0;
+                constexpr int split = decltype(splitc)::value;   // -1: all edges, else edges of parity
+                sfor<0, d>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int j = P::COL[e0 + k];
+                    constexpr int cidx = [] {
+                        int n = 0;
+                        for (int kk = 0; kk < k; ++kk) n += P::COL[e0 + kk] < KC;
+                        return n;
+                    }();
+                    if constexpr (j < KC && (split < 0 || cidx % NP == split)) {
+                        const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
+                        lds_T& acc = at(j * CS * TS + rot(gshift(e0 + k)));
+                        if constexpr (kFloodPlan<BG, T, NP, CS>.first_row[j] == i) {
+                            acc = T(0) + r;
+                        } else if constexpr (sizeof(T) == 8) {
+                            // ds_add_f64 without return: the LDS unit does the read-add-write (same
+                            // IEEE round-to-nearest double add), so a row group is not a chain of
+                            // dependent round trips (4.38 -> 4.17 ms per 4096 codeblocks).  The f32
+                            // ds_add_f32 measured 4x slower than read-add-write; f32 keeps the latter.
+                            __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        } else {
+                            acc = acc + r;
+                        }
+                    }
+                    asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
+                });
+            };
+            // the core LLRs of the LQ update, loaded now so phase B hides their latency
+            T lf[KH];
+            if (active)
+                sfor<0, KH>([&](auto jc) {
+                    constexpr int jj = decltype(jc)::value;
+                    const int j = h * KH + jj;
+                    if (j < KC) lf[jj] = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
+                });
+            sfor<0, kGroups<BG>.n>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                uint32_t csw[NPW];
+    #pragma unroll
+                for (int x = 0; x < NPW; ++x) csw[x] = nsw[x];
+                const T cA = qA, cB = qB;
+                const uint32_t cu = qu, cidx = qidx;
+                if constexpr (g + 1 < kGroups<BG>.n) {
+                    prefetch(std::integral_constant<int, g + 1>{});
+                    prefetch_state(std::integral_constant<int, g + 1>{});
+                }
+                auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                    const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
+                    return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
+                };
+                const bool gd = gdead(gc);   // a dead group adds nothing: no barrier either
+                if (active && !gd) {
+                    per_half([&](auto hc) {
+                        sfor<kGroups<BG>.start[g], kGroups<BG>.start[g + 1]>([&](auto ic) {
+                            constexpr int i = decltype(ic)::value;
+                            if (rdead(ic)) return;   // +-0 adds (a partly dead group)
+                            if constexpr (i < NLS) {   // LDS state: both halves, alternate edges
+                                rowB(ic, hc, gshift, cA, cB, cu, cidx);
+                            } else if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
+                                T a, b;
+                                uint32_t u, x;
+                                get_state(ic, a, b, u, x);
+                                rowB(ic, std::integral_constant<int, -1>{}, gshift, a, b, u, x);
+                            }
+                        });
+                    });
+                }
+                if (!gd) lds_barrier();
+            });
+            // ---- LQ = LLRin + sum (:126) for the own entries
+            if (active)
+                sfor<0, KH>([&](auto jc) {
+                    constexpr int jj = decltype(jc)::value;
+                    const int j = h * KH + jj;
+                    if (j < KC) {
+                        lds_T& x = own(j);
+                        x = lf[jj] + x;
+                    }
+                });
+        }
+        if (s == 0 && h == 0)
+            for (int c = 0; c < G; ++c) flagA[c] = 0;   // read before the phase-B barriers
+        if (!block_any(active)) break;
+    }
+
+    // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
+    zv = zg;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    auto rfinal = [&](auto ic, int k) -> T {
+        constexpr int i = decltype(ic)::value;
+        T a, b;
+        uint32_t u, idx;
+        get_state(ic, a, b, u, idx);
+        return xsign_v(pick(idx == (uint32_t)k, b, a), u << k, mv);
+    };
+    if (active) {
+        bool fail = false;
+        per_half([&](auto hc) {
+            sfor<0, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                constexpr int e0 = P::RS[i];
+                constexpr int d = P::RS[i + 1] - e0;
+                if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
+                    bool par = false;
+                    sfor<0, d>([&](auto kc) {
+                        constexpr int k = decltype(kc)::value;
+                        constexpr int j = P::COL[e0 + k];
+                        T a;
+                        if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                        else a = llrx(i) + rfinal(ic, k);
+                        par ^= (a <= T(0));
+                    });
+                    fail |= par;
+                }
+            });
+        });
+        if (fail) flagA[cl] = 1;
+    }
+    lds_barrier();
+    if (active) {
+        for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+        per_half([&](auto hc) {
+            sfor<4, MB>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+                if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
+                    crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
+            });
+        });
+        if (z == 0 && h == 0) {
+            status[out] = flagA[cl] == 0;
+            iters[out] = L;
+        }
+    }
+}
+
+#undef FP
+
+// NP parts x CS slots: 768 threads (3 waves per SIMD) for batches, 1024 (4 per SIMD) for the
+// 16-part configuration of small launches
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
+__global__ __launch_bounds__(NP * CS) __attribute__((amdgpu_waves_per_eu(NP * CS / 256))) void
+ldpc_flood_kernel(LDPC5G_DEC_PARAMS) {
+    flood_body<BG, T, OFS, NP, CS, DEAD>(LDPC5G_DEC_ARGS);
+}
+
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
+constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS, DEAD>; }
+
+template <int BG, typename T, int NP, int CS>
+size_t flood_lds_bytes() {
+    static_assert(flood_lds_bytes_t<BG, T, NP, CS>() <= kLdsPerCU, "LDS budget of one CU");
+    return flood_lds_bytes_t<BG, T, NP, CS>();
+}
+
+template <int BG, typename T, int NP, int CS, bool DEAD = false>
+int set_flood_lds(bool ofs) {
+    const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
+    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS, DEAD>()>(lds)
+               : set_lds_once<flood_kernel<BG, T, false, NP, CS, DEAD>()>(lds);
+}
+
+// G codeblocks per workgroup (G * Zc <= CS); NP parts of H = G*Zc rounded up to a wave
+template <int BG, typename T, int NP, int CS, bool DEAD = false>
+int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                     int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                     hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS, DEAD> : ldpc_flood_kernel<BG, T, false, NP, CS, DEAD>;
+    const int H = ((G * Zc + 63) / 64) * 64;
+    if (G < 1 || H > CS) return fail(LDPC5G_ESIZE, "flooding launch: %d codeblocks of Zc=%d per workgroup", G, Zc);
+    if (int rc = set_flood_lds<BG, T, NP, CS, DEAD>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
+    hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(NP * H), lds, st, llr, ck, status, iters, B, Zc,
+                       zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
+                       (const CbRef*)nullptr);
+    return check_hip(hipGetLastError(), "ldpc_flood_kernel launch");
+}
+
+constexpr int kFloodNP = 2, kFloodCS = kDecThreads;   // batch configuration: 2 x 384 slots
+constexpr int kFloodSmallNP = 16, kFloodSmallCS = 64;  // small launches: 16 x 64 slots
+
+template <int BG, typename T, bool DEAD = false>
+int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                   int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    // small batches (the per-codeblock drop-ins): no more slots than codeblocks
+    const int G = std::min(dec_G(Zc, false), B);
+    return launch_flood_cfg<BG, T, kFloodNP, kFloodCS, DEAD>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
+                                                             alpha, beta, pc, st);
+}
+
+template <int BG, typename T, bool DEAD = false>
+int launch_flood_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                         const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
+                         int pc, hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS, DEAD>
+                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS, DEAD>;
+    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS, DEAD>(ofs)) return rc;
+    const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodNP * kFloodCS), lds, st, llr, ck, status, iters, 0, 0,
+                       0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);
+    return check_hip(hipGetLastError(), "ldpc_flood_kernel(mixed) launch");
+}
+
+template <int BG, typename T>
+int flood_blocks_per_cu_t() {
+    const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
+    if (set_lds_once<flood_kernel<BG, T, false, kFloodNP, kFloodCS>()>(lds)) return -1;
+    int n = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS>,
+                                                     kFloodNP * kFloodCS, lds) != hipSuccess)
+        return -1;
+    return n;
+}
+
+}  // namespace
+}  // namespace ldpc5g_impl
