@@ -1,7 +1,8 @@
 """TS 38.212 §5.1 CRC attach / check — host-side mirror of py5gphy/crc/crc.py:4-88.
 
-Used by the codeblock-segmentation and DL-SCH host chain and by the BLER harness; the GPU
-CRC is a "next" item.  Same call surface: nr_crc_encode(blk, poly, mask=0)
+Per-block host drop-in (the reference's call surface) used by the per-codeblock host callers and
+the BLER harness.  The batched transport-channel chain computes its CRCs on the GPU instead
+(`ldpc5g_crc` / `tb_crc_kernel` / `tb_check_kernel`, sch.py).  Same call surface: nr_crc_encode(blk, poly, mask=0)
 -> int8 blk ++ crc, nr_crc_decode(blkandcrc, poly, mask=0) -> (blk, err).
 """
 import numpy as np

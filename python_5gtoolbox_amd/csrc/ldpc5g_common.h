@@ -153,6 +153,22 @@ int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uin
 int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int B, int Zc, int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha,
                        double beta, int pc, hipStream_t st);
+// float32 flooding instantiations, each in its own translation unit (parallel compiles)
+int flood_blocks_per_cu_f32(int bgn);
+int launch_flood_f32(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
+                     int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st);
+int launch_flood_mixed_f32(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                           const DecWork* work, const CbRef* cbs, int L, double alpha, double beta, int pc,
+                           hipStream_t st);
+int launch_flood_small_f32(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
+                           int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                           hipStream_t st);
+int launch_flood_dead_f32(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
+                          int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                          hipStream_t st);
+int launch_flood_mixed_dead_f32(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
+                                const DecWork* work, const CbRef* cbs, int L, double alpha, double beta, int pc,
+                                hipStream_t st);
 int launch_dec_mixed_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
                        double beta, int pc, hipStream_t st);

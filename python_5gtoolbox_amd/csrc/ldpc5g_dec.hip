@@ -1,5 +1,5 @@
-// ldpc5g_dec.hip — flooding min-sum decoder instantiations (float64: the drop-in's bit-exact path,
-// float32) and the decoder dispatch; the layered kernels live in ldpc5g_dec_l.hip.
+// ldpc5g_dec.hip — flooding min-sum decoder instantiations (float64: the drop-in's bit-exact path;
+// float32 in ldpc5g_dec_f32.hip) and the decoder dispatch; the layered kernels live in ldpc5g_dec_l.hip.
 // Part of libldpc5g.so (MI355X, gfx950).
 #include "ldpc5g_dec_flood.h"
 
@@ -8,7 +8,7 @@ namespace ldpc5g_impl {
 int dec_blocks_per_cu(int bgn, int dtype, bool layered) {
     if (layered) return dec_blocks_per_cu_l(bgn);
     if (dtype == LDPC5G_F64) return bgn == 1 ? flood_blocks_per_cu_t<1, double>() : flood_blocks_per_cu_t<2, double>();
-    return bgn == 1 ? flood_blocks_per_cu_t<1, float>() : flood_blocks_per_cu_t<2, float>();
+    return flood_blocks_per_cu_f32(bgn);
 }
 
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
@@ -27,9 +27,7 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
-    const float* p = (const float*)llr;
-    return bgn == 1 ? launch_flood_t<1, float>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
-                    : launch_flood_t<2, float>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    return launch_flood_f32(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
 }
 
 int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
@@ -45,9 +43,7 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }
-    const float* p = (const float*)llr;
-    return bgn == 1 ? launch_flood_mixed_t<1, float>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
-                    : launch_flood_mixed_t<2, float>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    return launch_flood_mixed_f32(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
 }
 
 }  // namespace ldpc5g_impl

@@ -164,6 +164,41 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// ---- ck through LDS (both decoders).  The decisions of a workgroup's slots are staged in LDS in
+// output order (byte j*Zc + z of slot s at s*SS, SS = Nf*Zc rounded up to 16) once the decoding is
+// over, then written as 16-B pieces of whole rows: every 128-B line of ck is written once and in
+// full (direct byte stores wrote 32-64 B per codeblock, column and wave).  A slot whose row is not
+// 16-B aligned (Zc % 4 != 0, or an odd ck offset) takes a byte loop, still one row per slot.
+__device__ __forceinline__ int ck_stage_stride(int NFZ) { return (NFZ + 15) & ~15; }
+__device__ __forceinline__ void ck_stage_byte(uint32_t off, uint32_t bit) {
+    *(__attribute__((address_space(3))) uint8_t*)(uintptr_t)off = (uint8_t)bit;
+}
+__device__ __forceinline__ bool ck_row_aligned(int NFZ, const int8_t* p) {
+    return (NFZ & 15) == 0 && ((uintptr_t)p & 15) == 0;
+}
+// after the staging writes and a barrier; `slow`: some slot's row is unaligned (workgroup-uniform)
+template <typename SlotDst>
+__device__ __forceinline__ void ck_store_staged(int NFZ, int nslots, SlotDst&& slot_dst, bool slow,
+                                                int t, int nthr) {
+    using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+    using lds_u4 = __attribute__((address_space(3))) u32x4;
+    using lds_u8 = __attribute__((address_space(3))) uint8_t;
+    const int SS = ck_stage_stride(NFZ);
+    const int nch = NFZ >> 4;
+    for (int c = t; c < nslots * nch; c += nthr) {
+        const int s = c / nch, k = c - s * nch;
+        int8_t* dst = slot_dst(s);
+        if (ck_row_aligned(NFZ, dst)) *(u32x4*)(dst + 16 * k) = *(lds_u4*)(uintptr_t)(uint32_t)(s * SS + 16 * k);
+    }
+    if (slow) {
+        for (int c = t; c < nslots * NFZ; c += nthr) {
+            const int s = c / NFZ, b = c - s * NFZ;
+            int8_t* dst = slot_dst(s);
+            if (!ck_row_aligned(NFZ, dst)) dst[b] = (int8_t)*(lds_u8*)(uintptr_t)(uint32_t)(s * SS + b);
+        }
+    }
+}
+
 // OFS = false: the caller guarantees beta == 0 (plain / normalized min-sum), so the offset and
 // its clamp at 0 are compiled out (min >= +0 already; the result is identical).
 // DEAD = true: the variant for rate-recovered inputs (LDPC5G_RATE_MATCHED), which detects and
@@ -185,6 +220,7 @@ __device__ __forceinline__ void dec_body(
     constexpr int NLR = lds_rows<BG>();
     constexpr int FLAG_B = ST_B + 2 * NLR * CS * TS;
     constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // wrap table, 2*CS entries
+    static_assert(FLAG_B >= CS * P::NB + 15 * kMaxG, "ck staging (G * SS bytes) below the flags");
     extern __shared__ __align__(16) unsigned char smem[];
 
     if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
@@ -307,13 +343,22 @@ __device__ __forceinline__ void dec_body(
     uint64_t hdx_prev = 0;   // ... of own extension columns
     uint64_t nzx = 0;        // extension columns whose LLR is not +0.0 (bit pattern) at this z
     if (valid) {
+        // all Nf - pc loads are issued before any is used: one HBM round trip per workgroup
+        // (a conditional load per punctured column made 26 + 6 dependent round trips, ~40 us)
+        T vc[KC], vx[MB - 4];
+#pragma unroll
+        for (int j = 0; j < KC; ++j) vc[j] = lrow[(j < pc ? 0 : j - pc) * Zc + z];
+#pragma unroll
+        for (int i4 = 0; i4 < MB - 4; ++i4) vx[i4] = lrow[(KB + 4 + i4 - pc) * Zc + z];
+#pragma unroll
         for (int j = 0; j < KC; ++j) {
-            const T v = j < pc ? T(0) : lrow[(j - pc) * Zc + z];   // punctured columns: LLR 0 (:43)
+            const T v = j < pc ? T(0) : vc[j];   // punctured columns: LLR 0 (:43)
             own(j) = v;
             hdc_prev |= (uint32_t)(v < T(0)) << j;
         }
+#pragma unroll
         for (int i4 = 0; i4 < MB - 4; ++i4) {
-            const T v = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            const T v = vx[i4];
             hdx_prev |= (uint64_t)(v < T(0)) << i4;
             nzx |= (uint64_t)(FT<T>::bits(v) != 0) << i4;
         }
@@ -558,8 +603,8 @@ __device__ __forceinline__ void dec_body(
             if (active)
                 for (int j = 0; j < KC; ++j) hdc |= (uint32_t)(own(j) < T(0)) << j;
             if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;
-            hdc_prev = hdc;
-            hdx_prev = hdx;
+            // a stopped slot keeps the decisions of its stopping iteration (staged at the end)
+            if (active) hdc_prev = hdc, hdx_prev = hdx;
             lds_barrier();
             const bool cand = active && flagA[cl] == 0;
             if (block_any(cand)) {
@@ -584,9 +629,6 @@ __device__ __forceinline__ void dec_body(
                 }
                 lds_barrier();
                 if (cand && flagB[cl] == 0) {
-                    for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)((hdc >> j) & 1u);
-                    for (int i4 = 0; i4 < MB - 4; ++i4)
-                        crow[(KB + 4 + i4) * Zc + zv] = (int8_t)((hdx >> i4) & 1u);
                     if (z == 0) status[out] = 1, iters[out] = it + 1;
                     active = false;
                 }
@@ -606,7 +648,14 @@ __device__ __forceinline__ void dec_body(
     zv = z;
     asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
     if (active) {
+        // every extension LLR is requested before the pass uses any: one round trip, not one per
+        // row (the scheduler serialised them under the pass's register pressure: ~30 us per WG)
+        T vx[MB - 4];
+#pragma unroll
+        for (int i4 = 0; i4 < MB - 4; ++i4) vx[i4] = llrx(i4);
+        __builtin_amdgcn_sched_barrier(0);
         bool fail = false;
+        uint64_t ox = 0;
         sfor<0, MB>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             constexpr int e0 = P::RS[i];
@@ -616,27 +665,42 @@ __device__ __forceinline__ void dec_body(
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
                 T a;
-                if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
-                else a = llrx(i - 4) + rfinal(ic, d, k);
+                if constexpr (j < KC) {
+                    a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                } else {
+                    a = vx[i - 4] + rfinal(ic, d, k);
+                    ox |= (uint64_t)(a <= T(0)) << (i - 4);
+                }
                 par ^= (a <= T(0));
             });
             fail |= par;
         });
         if (fail) flagA[cl] = 1;
+        uint32_t oc = 0;
+        for (int j = 0; j < KC; ++j) oc |= (uint32_t)(own(j) <= T(0)) << j;
+        hdc_prev = oc, hdx_prev = ox;
     }
-    lds_barrier();
-    if (active) {
-        for (int j = 0; j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
-        sfor<4, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
-            const T a = llrx(i - 4) + rfinal(ic, dl + 1, dl);
-            crow[(KB + i) * Zc + zv] = (int8_t)(a <= T(0));
-        });
-        if (z == 0) {
-            status[out] = flagA[cl] == 0;
-            iters[out] = L;
+    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here
+    if (active && z == 0) {
+        status[out] = flagA[cl] == 0;
+        iters[out] = L;
+    }
+    // ---- ck through LDS (ck_store_staged): LDS below FLAG_B is free, and G * SS <= 768 * Nf + 15 * G
+    //      fits it for every Zc
+    {
+        const int NFZ = P::NB * Zc;
+        if (valid) {
+            const uint32_t sb = (uint32_t)(cl * ck_stage_stride(NFZ) + zv);
+            for (int j = 0; j < KC; ++j) ck_stage_byte(sb + (uint32_t)(j * Zc), (hdc_prev >> j) & 1u);
+            for (int i4 = 0; i4 < MB - 4; ++i4)
+                ck_stage_byte(sb + (uint32_t)((KB + 4 + i4) * Zc), (uint32_t)(hdx_prev >> i4) & 1u);
         }
+        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow));   // orders the staging too
+        const int nslots = work ? G : min(G, B - (int)blockIdx.x * G);
+        ck_store_staged(NFZ, nslots, [&](int sl) -> int8_t* {
+            if (work) return ck + cbs[work[blockIdx.x].first + sl].ck_off;
+            return ck + (int64_t)((int)blockIdx.x * G + sl) * ldc;
+        }, slow, t, (int)blockDim.x);
     }
 }
 

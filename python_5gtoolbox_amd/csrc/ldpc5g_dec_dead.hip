@@ -1,6 +1,6 @@
 // ldpc5g_dec_dead.hip — the flooding decoder's dead-extension-row variants (DEAD = true, float64
-// and float32, batch and mixed work lists), selected by LDPC5G_RATE_MATCHED.
-// Own translation unit: compiles in parallel with the plain instantiations (ldpc5g_dec.hip).
+// batch and mixed work lists), selected by LDPC5G_RATE_MATCHED: float64 here,
+// float32 in ldpc5g_dec_dead_f32.hip.  Own translation units: they compile in parallel.
 #include "ldpc5g_dec_flood.h"
 
 namespace ldpc5g_impl {
@@ -13,9 +13,7 @@ int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* 
         return bgn == 1 ? launch_flood_t<1, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
-    const float* p = (const float*)llr;
-    return bgn == 1 ? launch_flood_t<1, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
-                    : launch_flood_t<2, float, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    return launch_flood_dead_f32(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
 }
 
 int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
@@ -26,9 +24,8 @@ int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uin
         return bgn == 1 ? launch_flood_mixed_t<1, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }
-    const float* p = (const float*)llr;
-    return bgn == 1 ? launch_flood_mixed_t<1, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
-                    : launch_flood_mixed_t<2, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+    return launch_flood_mixed_dead_f32(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc,
+                                       st);
 }
 
 }  // namespace ldpc5g_impl

@@ -293,7 +293,17 @@ __device__ __forceinline__ void flood_body(
     // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS row state 0; wrap table
     uint64_t nzx = 0;   // extension columns of this half's rows whose LLR is not +0.0 at this z
     if (valid) {
-        for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) own(j) = j < pc ? T(0) : lrow[(j - pc) * Zc + z];
+        // all loads issued before any is used: one HBM round trip (a conditional load per
+        // punctured column made KH dependent round trips per workgroup)
+        T v0[KH];
+        sfor<0, KH>([&](auto jc) {
+            const int j = min(h * KH + decltype(jc)::value, KC - 1);
+            v0[decltype(jc)::value] = lrow[(j < pc ? 0 : j - pc) * Zc + z];
+        });
+        sfor<0, KH>([&](auto jc) {
+            const int j = h * KH + decltype(jc)::value;
+            if (j < KC) own(j) = j < pc ? T(0) : v0[decltype(jc)::value];
+        });
         if constexpr (DEAD)
             per_half_init([&](auto hc) {
                 sfor<4, MB>([&](auto ic) {
@@ -361,6 +371,7 @@ __device__ __forceinline__ void flood_body(
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
     asm volatile("" : "+v"(mv));
 
+    uint64_t hdx_keep = 0;   // extension decisions of a slot decided by the syndrome test
     int it = 0;
     for (; it < L; ++it) {
         // zv / ziv opaque per iteration: otherwise LICM hoists the ~300 loop-invariant shift
@@ -511,14 +522,9 @@ __device__ __forceinline__ void flood_body(
         prefetch_state(std::integral_constant<int, 0>{});
         // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
         if (active && flagA[cl] == 0) {
-            for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) < T(0));
-            per_half([&](auto hc) {
-                sfor<4, MB>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
-                        crow[(KB + i) * Zc + zv] = (int8_t)((hdx >> (i - 4)) & 1u);
-                });
-            });
+            // decided: its LQ entries stay frozen in LDS (no phase B / LQ update for an inactive
+            // slot) and its extension decisions are kept, for the staged ck store at the end
+            hdx_keep = hdx;
             if (z == 0 && h == 0) status[out] = 1, iters[out] = it;
             active = false;
         }
@@ -561,7 +567,8 @@ __device__ __forceinline__ void flood_body(
             sfor<0, KH>([&](auto jc) {
                 constexpr int jj = decltype(jc)::value;
                 const int j = h * KH + jj;
-                if (j < KC) lf[jj] = j < pc ? T(0) : lrow[(j - pc) * Zc + zv];
+                const int jl = min(j, KC - 1);   // unconditional: all loads in flight at once
+                lf[jj] = lrow[(jl < pc ? 0 : jl - pc) * Zc + zv];
             });
         sfor<0, kGroups<BG>.n>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
@@ -604,7 +611,7 @@ __device__ __forceinline__ void flood_body(
                 const int j = h * KH + jj;
                 if (j < KC) {
                     lds_T& x = own(j);
-                    x = lf[jj] + x;
+                    x = (j < pc ? T(0) : lf[jj]) + x;   // punctured columns: LLR 0 (:43)
                 }
             });
         if (s == 0 && h == 0)
@@ -622,8 +629,25 @@ __device__ __forceinline__ void flood_body(
         get_state(ic, a, b, u, idx);
         return xsign_v(pick(idx == (uint32_t)k, b, a), u << k, mv);
     };
+    uint32_t oc = 0;          // own core columns (bit j - h*KH): LQ <= 0, or LQ_old < 0 if decided
+    uint64_t ox = hdx_keep;   // own extension columns
     if (active) {
+        // the owned rows' extension LLRs are all requested before the pass uses any (one round trip)
+        constexpr int NXMAX = [] {
+            int m = 0;
+            for (int p = 0; p < NP; ++p) m = m > kFloodPlan<BG, T, NP, CS>.nx[p] ? m : kFloodPlan<BG, T, NP, CS>.nx[p];
+            return m;
+        }();
+        T vx[NXMAX > 0 ? NXMAX : 1];
+        per_half([&](auto hc) {
+            constexpr int hh = decltype(hc)::value;
+            sfor<0, kFloodPlan<BG, T, NP, CS>.nx[hh]>([&](auto pc_) {
+                vx[decltype(pc_)::value] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][decltype(pc_)::value]);
+            });
+        });
+        __builtin_amdgcn_sched_barrier(0);
         bool fail = false;
+        ox = 0;
         per_half([&](auto hc) {
             sfor<0, MB>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
@@ -635,8 +659,12 @@ __device__ __forceinline__ void flood_body(
                         constexpr int k = decltype(kc)::value;
                         constexpr int j = P::COL[e0 + k];
                         T a;
-                        if constexpr (j < KC) a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
-                        else a = llrx(i) + rfinal(ic, k);
+                        if constexpr (j < KC) {
+                            a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
+                        } else {
+                            a = vx[kFloodPlan<BG, T, NP, CS>.xpos[i]] + rfinal(ic, k);
+                            ox |= (uint64_t)(a <= T(0)) << (i - 4);
+                        }
                         par ^= (a <= T(0));
                     });
                     fail |= par;
@@ -645,21 +673,48 @@ __device__ __forceinline__ void flood_body(
         });
         if (fail) flagA[cl] = 1;
     }
-    lds_barrier();
-    if (active) {
-        for (int j = h * KH; j < (h + 1) * KH && j < KC; ++j) crow[j * Zc + zv] = (int8_t)(own(j) <= T(0));
+    if (valid)
+        sfor<0, KH>([&](auto jc) {
+            const int j = h * KH + decltype(jc)::value;
+            if (j < KC) {
+                const T v = own(j);
+                oc |= (uint32_t)(active ? v <= T(0) : v < T(0)) << decltype(jc)::value;
+            }
+        });
+    lds_barrier();   // every LQ / state read is done: LDS below FLAG_B is free from here
+    if (active && z == 0 && h == 0) {
+        status[out] = flagA[cl] == 0;
+        iters[out] = L;
+    }
+    // ---- ck through LDS (ck_store_staged, ldpc5g_dec_body.h); direct byte stores when the
+    //      workgroup's rows exceed the space below the flags (small-CS configurations)
+    const int NFZ = P::NB * Zc;
+    const bool staged = G * ck_stage_stride(NFZ) <= FLAG_B;
+    if (valid) {
+        const uint32_t sb = (uint32_t)(cl * ck_stage_stride(NFZ) + zv);
+        auto put = [&](int col, uint32_t bit) {
+            if (staged) ck_stage_byte(sb + (uint32_t)(col * Zc), bit);
+            else crow[col * Zc + zv] = (int8_t)bit;
+        };
+        sfor<0, KH>([&](auto jc) {
+            const int j = h * KH + decltype(jc)::value;
+            if (j < KC) put(j, (oc >> decltype(jc)::value) & 1u);
+        });
         per_half([&](auto hc) {
             sfor<4, MB>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
                 if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value)
-                    crow[(KB + i) * Zc + zv] = (int8_t)(llrx(i) + rfinal(ic, dl) <= T(0));
+                    put(KB + i, (uint32_t)(ox >> (i - 4)) & 1u);
             });
         });
-        if (z == 0 && h == 0) {
-            status[out] = flagA[cl] == 0;
-            iters[out] = L;
-        }
+    }
+    if (staged) {
+        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow));   // orders the staging too
+        const int nslots = work ? G : min(G, B - (int)blockIdx.x * G);
+        ck_store_staged(NFZ, nslots, [&](int sl) -> int8_t* {
+            if (work) return ck + cbs[work[blockIdx.x].first + sl].ck_off;
+            return ck + (int64_t)((int)blockIdx.x * G + sl) * ldc;
+        }, slow, t, (int)blockDim.x);
     }
 }
 

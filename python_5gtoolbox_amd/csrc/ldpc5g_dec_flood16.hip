@@ -1,7 +1,8 @@
 // ldpc5g_dec_flood16.hip — the flooding decoder's small-launch configuration: 16 parts x 64 slots
 // (1024 threads) share the base rows of at most 64 slots' codeblocks, e.g. ONE BG2 Zc=8 codeblock
 // per call from the per-codeblock drop-ins (BASELINE config 1), where the batch configuration's two
-// parts leave each wave a long serial row chain.  Own translation unit: compiles in parallel.
+// parts leave each wave a long serial row chain.  float64 here, float32 in ldpc5g_dec_flood16_f32.hip
+// (own translation units: they compile in parallel).
 #include "ldpc5g_dec_flood.h"
 
 namespace ldpc5g_impl {
@@ -15,9 +16,8 @@ int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t*
         return bgn == 1 ? launch_flood_cfg<1, double, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_cfg<2, double, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
     }
-    const float* p = (const float*)llr;
-    return bgn == 1 ? launch_flood_cfg<1, float, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st)
-                    : launch_flood_cfg<2, float, NP, CS>(p, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
+    return launch_flood_small_f32(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta,
+                                  pc, st);
 }
 
 }  // namespace ldpc5g_impl

@@ -403,20 +403,39 @@ __device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double
 // times holds (0.0 + v_0 + ... + v_{cnt-1}) / cnt (the row-by-row numpy sum of tmp_buf);
 // unvisited positions 0; fillers 10 * max|LLR| of the codeblock.  A float32 output is the
 // float64 result rounded once.
-template <typename Tin, typename Tout>
+// STAGE: the codeblock's E input LLRs are first copied into LDS in de-interleaved order
+// (lds[q*EQ + r] = llr[r*Qm + q], i.e. lds[k] is the k-th bit of the interleaver's column read-out),
+// in the same pass as the max|LLR| reduction: the input is read once, coalesced, and the gather
+// below reads LDS at consecutive k instead of global memory at stride Qm.  Without STAGE (E too
+// large for LDS) the gather reads global memory.  Outputs: 4 consecutive positions per thread,
+// stored as 16-B pieces when the row is 16-B aligned.
+template <typename Tin, typename Tout, bool STAGE>
 __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restrict__ llr, int64_t ldg,
                                                             SchDev s0, const SchGeo* __restrict__ gv,
                                                             const RowRef* __restrict__ rm,
                                                             const Tout* __restrict__ harq,
                                                             Tout* __restrict__ out) {
     __shared__ double red[kRrNT / 64];
+    extern __shared__ __align__(16) unsigned char rr_smem[];
+    Tin* lk = (Tin*)rr_smem;
     const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, 0);
     const SchDev& s = rg.s;
     const int t = rg.t, c = rg.c;
     const int E = cb_E(s, c), EQ = E / s.Qm;
     const Tin* fe = llr + (int64_t)t * ldg + cb_goff(s, c);
     double m = 0.0;
-    for (int e = threadIdx.x; e < E; e += kRrNT) m = fmax(m, fabs(ld64(fe, e)));
+    if constexpr (STAGE) {
+        for (int r = threadIdx.x; r < EQ; r += kRrNT) {
+            const Tin* src = fe + (int64_t)r * s.Qm;
+            for (int q = 0; q < s.Qm; ++q) {
+                const Tin x = src[q];
+                lk[q * EQ + r] = x;
+                m = fmax(m, fabs((double)x));
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < E; e += kRrNT) m = fmax(m, fabs(ld64(fe, e)));
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -427,7 +446,7 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     const double mx = m * 10.0;
     const int64_t row = rg.dn_row;
     const int qE = E / s.size, rE = E - qE * s.size;   // visits of rank rr: qE + (rr < rE)
-    for (int p = threadIdx.x; p < s.N; p += kRrNT) {
+    auto value = [&](int p) -> double {
         double v = 0.0;
         if (p >= s.f0 && p < s.f0 + s.F) {
             v = mx;
@@ -439,7 +458,8 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
                 double acc = 0.0;
                 for (int j = 0; j < cnt; ++j) {
                     const int k = rr + j * s.size;
-                    acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
+                    if constexpr (STAGE) acc += (double)lk[k];
+                    else acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
                 }
                 v = cnt == 1 ? acc : acc / (double)cnt;   // x / 1.0 == x: skip the f64 divide
             }
@@ -448,7 +468,28 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
             const double h = (double)harq[row + p];
             v = (v == 0.0 || h == 0.0) ? v + h : (v + h) / 2.0;
         }
-        out[row + p] = (Tout)v;
+        return v;
+    };
+    Tout* orow = out + row;
+    const bool vec = ((uintptr_t)orow & 15) == 0;
+    for (int p0 = 4 * (int)threadIdx.x; p0 < s.N; p0 += 4 * kRrNT) {
+        Tout v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = p0 + q < s.N ? (Tout)value(p0 + q) : Tout(0);
+        if (vec && p0 + 4 <= s.N) {
+            if constexpr (sizeof(Tout) == 4) {
+                using f4 = float __attribute__((ext_vector_type(4)));
+                *(f4*)(orow + p0) = f4{v[0], v[1], v[2], v[3]};
+            } else {
+                using d2 = double __attribute__((ext_vector_type(2)));
+                *(d2*)(orow + p0) = d2{v[0], v[1]};
+                *(d2*)(orow + p0 + 2) = d2{v[2], v[3]};
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (p0 + q < s.N) orow[p0 + q] = v[q];
+        }
     }
 }
 
@@ -526,18 +567,33 @@ int64_t sch_total_E(const SchDev& s) {
     return (int64_t)s.c_switch * s.E_lo + (int64_t)(s.C - s.c_switch) * s.E_hi;
 }
 
+// the E LLRs of a codeblock are staged in LDS up to this size (4 x 512-thread workgroups per CU)
+constexpr int kRrStageBytes = 40 * 1024;
+
+template <typename Tin, typename Tout>
+void raterecover_go(dim3 grid, const void* llr, int64_t ldg, const SchDev& s, const SchGeo* gv,
+                    const RowRef* rm, const void* harq_in, void* llr_dn, int max_cb_E, hipStream_t st) {
+    const size_t lds = (size_t)max_cb_E * sizeof(Tin);
+    if (lds <= (size_t)kRrStageBytes)
+        hipLaunchKernelGGL((raterecover_kernel<Tin, Tout, true>), grid, dim3(kRrNT), lds, st, (const Tin*)llr, ldg, s,
+                           gv, rm, (const Tout*)harq_in, (Tout*)llr_dn);
+    else
+        hipLaunchKernelGGL((raterecover_kernel<Tin, Tout, false>), grid, dim3(kRrNT), 0, st, (const Tin*)llr, ldg, s,
+                           gv, rm, (const Tout*)harq_in, (Tout*)llr_dn);
+}
+
+// max_cb_E: the largest per-codeblock E of the launch (sizes the LDS stage)
 int launch_raterecover(dim3 grid, const void* llr, int llr_dtype, int64_t ldg, const SchDev& s,
                        const SchGeo* gv, const RowRef* rm, const void* harq_in, void* llr_dn,
-                       int dn_dtype, hipStream_t st) {
-    const dim3 blk(kRrNT);
+                       int dn_dtype, int max_cb_E, hipStream_t st) {
     if (llr_dtype == LDPC5G_F32 && dn_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<float, float>), grid, blk, 0, st, (const float*)llr, ldg, s, gv, rm, (const float*)harq_in, (float*)llr_dn);
+        raterecover_go<float, float>(grid, llr, ldg, s, gv, rm, harq_in, llr_dn, max_cb_E, st);
     else if (llr_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<float, double>), grid, blk, 0, st, (const float*)llr, ldg, s, gv, rm, (const double*)harq_in, (double*)llr_dn);
+        raterecover_go<float, double>(grid, llr, ldg, s, gv, rm, harq_in, llr_dn, max_cb_E, st);
     else if (dn_dtype == LDPC5G_F32)
-        hipLaunchKernelGGL((raterecover_kernel<double, float>), grid, blk, 0, st, (const double*)llr, ldg, s, gv, rm, (const float*)harq_in, (float*)llr_dn);
+        raterecover_go<double, float>(grid, llr, ldg, s, gv, rm, harq_in, llr_dn, max_cb_E, st);
     else
-        hipLaunchKernelGGL((raterecover_kernel<double, double>), grid, blk, 0, st, (const double*)llr, ldg, s, gv, rm, (const double*)harq_in, (double*)llr_dn);
+        raterecover_go<double, double>(grid, llr, ldg, s, gv, rm, harq_in, llr_dn, max_cb_E, st);
     return check_hip(hipGetLastError(), "raterecover launch");
 }
 
@@ -732,7 +788,8 @@ int ldpc5g_sch_raterecover(const void* llr, int32_t llr_dtype, int64_t ldg,
     if (T == 0) return LDPC5G_OK;
     if (!llr || !llr_dn) return fail(LDPC5G_ESIZE, "null buffer");
     hipStream_t st = (hipStream_t)stream;
-    return launch_raterecover(dim3(T * s.C), llr, llr_dtype, ldg, s, nullptr, nullptr, harq_in, llr_dn, dn_dtype, st);
+    return launch_raterecover(dim3(T * s.C), llr, llr_dtype, ldg, s, nullptr, nullptr, harq_in, llr_dn, dn_dtype,
+                              std::max(s.E_lo, s.E_hi), st);
 }
 
 int ldpc5g_sch_tb_check(const int8_t* ck, int64_t ldc, const ldpc5g_sch_cfg_t* cfg, int32_t T,
@@ -836,8 +893,10 @@ int ldpc5g_sch_decode_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
     if (int rc = m.upload(st)) return rc;
     const SchDev s0{};
     const int rows = (int)m.rows.size();
+    int max_cb_E = 0;
+    for (const SchGeo& g : m.geo) max_cb_E = std::max(max_cb_E, std::max(g.s.E_lo, g.s.E_hi));
     if (int rc = launch_raterecover(dim3(rows), llr, llr_dtype, ldg, s0, m.dgeo(), m.drows(), harq_in, llr_dn,
-                                    dn_dtype, st))
+                                    dn_dtype, max_cb_E, st))
         return rc;
     // every codeblock with its own (bgn, Zc): the mixed-Zc decoder (<= 2 launches)
     std::vector<ldpc5g_cb_desc_t> desc(rows);

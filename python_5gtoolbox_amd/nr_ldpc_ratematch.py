@@ -1,6 +1,7 @@
 """LDPC rate matching (TS 38.212 §5.4.2) — mirror of py5gphy/ldpc/nr_ldpc_ratematch.py:5-97.
 
-Host-side caller of the encoder (GPU rate matching is SURVEY §8(f) item f2)."""
+Per-codeblock host drop-in (the reference's call surface) around the GPU encoder.  Batched GPU
+rate matching is `ratematch_kernel` (`ldpc5g_sch_ratematch`, sch.py)."""
 import math
 
 import numpy as np

@@ -1,7 +1,9 @@
 """LDPC rate recovery (inverse of §5.4.2) — mirror of py5gphy/ldpc/nr_ldpc_raterecover.py:6-65.
 
 Produces the decoder input LLRs: de-interleave, average repeated transmissions, 0 for
-punctured bits, 10*max|LLR| on filler positions.  Host-side (GPU version: SURVEY §8(f) f1)."""
+punctured bits, 10*max|LLR| on filler positions.  Per-codeblock host drop-in (the reference's
+call surface); the batched GPU rate recovery + HARQ combining is `raterecover_kernel`
+(`ldpc5g_sch_raterecover`, sch.py)."""
 import numpy as np
 
 

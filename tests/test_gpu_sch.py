@@ -159,6 +159,41 @@ def test_raterecover_vs_reference_golden(torch, sch):
         assert np.array_equal(out32, rr.astype(np.float32)), i   # float64 result rounded once
 
 
+@pytest.mark.parametrize("args", [
+    (2000, 2, 500, 1, 0, 60000, 60000),     # one codeblock, E = 60000 > Ncb: repetitions, no LDS stage
+    (200, 2, 300, 1, 0, 60000, 3000),       # E > Ncb with the E LLRs staged in LDS (repetitions)
+    (24000, 8, 900, 1, 2, 60000, 27000),    # E = 9000 per codeblock: f32 staged in LDS, f64 not
+    (8000, 4, 700, 1, 3, 60000, 4000),      # small E: staged for both input dtypes
+    (3000, 6, 300, 1, 1, 60000, 6000),      # Qm = 6 (de-interleave by 6)
+])
+def test_raterecover_stage_paths_vs_oracle(torch, sch, args):
+    """raterecover_kernel's LDS-staged gather (E * sizeof(llr) <= 40 KB) and its global-memory
+    gather, float32 / float64 in and out, T = 3 TBs, HARQ combining: == oracle.sch_raterecover
+    (float64 bit-exact; float32 output = the float64 result rounded once)."""
+    rng = np.random.default_rng(args[0])
+    cfg = sch.sch_config(*args)
+    p = O.sch_params(*args)
+    T = 3
+    llr = rng.normal(0, 4, (T, args[6]))
+    llr[:, ::7] = 0.0
+    harq = rng.normal(0, 2, (T * cfg.C, cfg.N))
+    harq[:, ::5] = 0.0
+    assert O.sch_params(*args)["C"] == cfg.C
+    for tin in (torch.float64, torch.float32):
+        x = torch.from_numpy(llr).cuda().to(tin)
+        xin = x.double().cpu().numpy()
+        ref = np.concatenate([O.sch_raterecover(xin[t], p) for t in range(T)])
+        refh = np.where((ref == 0) | (harq == 0), ref + harq, (ref + harq) / 2.0)
+        for tout in (torch.float64, torch.float32):
+            out = sch.sch_raterecover_batch(x, cfg, dn_dtype=tout).cpu().numpy()
+            assert np.array_equal(out, ref.astype(out.dtype)), (tin, tout)
+            h = torch.from_numpy(harq).cuda().to(tout)
+            hv = h.double().cpu().numpy()   # the kernel combines in float64, rounds once
+            exp = np.where((ref == 0) | (hv == 0), ref + hv, (ref + hv) / 2.0).astype(out.dtype)
+            outh = sch.sch_raterecover_batch(x, cfg, harq_in=h, dn_dtype=tout).cpu().numpy()
+            assert np.array_equal(outh, exp), (tin, tout, "harq")
+
+
 # ------------------------------------------------------------------------------ decode chain
 def test_sch_golden_decode_dropins(torch, gold):
     from python_5gtoolbox_amd import nr_dlsch_decode, nr_ulsch_decode

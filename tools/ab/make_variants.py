@@ -202,6 +202,30 @@ VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
                  "lay_pre12": (LAYERED, _pre(12))})
 
 
+# instrumentation (wrong ck rows): thread 0 of every workgroup records the real-time clock (100 MHz)
+# at 6 points — start, after the prologue, after iteration 1, loop exit, after the final syndrome
+# pass, after the ck store — into the first 48 bytes of its first codeblock's ck row
+# (tools/ts_probe.py reads them): where a workgroup's fixed (per-launch, not per-iteration) time goes
+_TS = [
+    ("    const int t = threadIdx.x;\n    if (work) {\n        DecWork w = work[blockIdx.x];",
+     "    const int t = threadIdx.x;\n    uint64_t ts[6];\n    ts[0] = __builtin_amdgcn_s_memrealtime();\n"
+     "    if (work) {\n        DecWork w = work[blockIdx.x];"),
+    ("    bool active = valid;\n    lds_barrier();\n",
+     "    bool active = valid;\n    lds_barrier();\n    ts[1] = __builtin_amdgcn_s_memrealtime();\n"),
+    ("        if (!block_any(active)) break;\n    }\n",
+     "        if (it == 0) ts[2] = __builtin_amdgcn_s_memrealtime();\n        if (!block_any(active)) break;\n    }\n"
+     "    ts[3] = __builtin_amdgcn_s_memrealtime();\n"),
+    ("    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here\n",
+     "    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here\n"
+     "    ts[4] = __builtin_amdgcn_s_memrealtime();\n"),
+    ("        }, slow, t, (int)blockDim.x);\n    }\n}\n",
+     "        }, slow, t, (int)blockDim.x);\n    }\n    __syncthreads();\n    ts[5] = __builtin_amdgcn_s_memrealtime();\n"
+     "    if (t == 0 && !work) {\n        uint64_t* o = (uint64_t*)(ck + (int64_t)((int)blockIdx.x * G) * ldc);\n"
+     "        for (int k = 0; k < 6; ++k) o[k] = ts[k];\n    }\n}\n"),
+]
+VARIANTS.update({"lay_ts": (LAYERED, _TS)})
+
+
 def make(name):
     target, patches = VARIANTS[name]
     d = os.path.join(ROOT, "build", "alt_src", name)

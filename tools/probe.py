@@ -61,9 +61,10 @@ def main():
             sched = what
             if what == "flooding64":   # the reference-exact float64 flooding mode
                 llr, sched = llr.double(), "flooding"
-            ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, BG, 8, "min-sum", 0.75, 0.0, sched,
+            L = int(os.environ.get("PROBE_L", "8"))
+            ms = timeit(lambda: D.nr_decode_ldpc_batch(llr, ZC, BG, L, "min-sum", 0.75, 0.0, sched,
                                                        out=out), 5)
-            print(f"{what} B={B}: {ms:.3f} ms  {B / ms / 1e3:.3f} M CB/s  iters "
+            print(f"{what} L={L} B={B}: {ms:.3f} ms  {B / ms / 1e3:.3f} M CB/s  iters "
                   f"{out[2].float().mean().item():.2f}")
 
 
