@@ -164,6 +164,85 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// ---- syndrome passes (final status, layered stop rule): the rows of ROWS in batches of <= 32 core
+// edges, every rotated APP read of a batch issued before any is compared.  Written edge by edge, the
+// compiler waited for each read before the next (s_waitcnt per edge: ~15 us per workgroup, 40 % of
+// an iteration, for a pass with 1/3 of an iteration's instructions).
+template <int BG>
+constexpr int core_deg(int i) {
+    int c = 0;
+    for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i + 1]; ++e) c += BGT<BG>::COL[e] < BGT<BG>::KC;
+    return c;
+}
+template <int BG, uint64_t ROWS>
+struct SynPlan {
+    int n = 0;
+    int r0[64] = {}, r1[64] = {};
+    constexpr SynPlan() {
+        int e = 0;
+        bool open = false;
+        for (int i = 0; i < BGT<BG>::MB; ++i) {
+            if (!((ROWS >> i) & 1u)) continue;
+            const int c = core_deg<BG>(i);
+            if (open && e + c > 32) r1[n++] = i, open = false;
+            if (!open) r0[n] = i, e = 0, open = true;
+            e += c;
+        }
+        if (open) r1[n++] = BGT<BG>::MB;
+    }
+};
+template <int BG, uint64_t ROWS>
+constexpr SynPlan<BG, ROWS> kSynPlan{};
+// slot of core edge k of row i among the core edges of ROWS rows in [r0, i) + row i's first k
+template <int BG, uint64_t ROWS>
+constexpr int syn_slot(int r0, int i, int k) {
+    int n = 0;
+    for (int r = r0; r < i; ++r)
+        if ((ROWS >> r) & 1u) n += core_deg<BG>(r);
+    for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i] + k; ++e) n += BGT<BG>::COL[e] < BGT<BG>::KC;
+    return n;
+}
+// true when some row of ROWS fails: parity over its core edges of (core(ic, kc) < 0) [STRICT] or
+// (<= 0), XOR ext(ic) (the decision of the row's extension edge; rows >= 4 only)
+template <int BG, uint64_t ROWS, bool STRICT, typename T, typename Core, typename Ext>
+__device__ __forceinline__ bool syndrome_fails(Core&& core, Ext&& ext) {
+    using P = BGT<BG>;
+    bool fail = false;
+    sfor<0, kSynPlan<BG, ROWS>.n>([&](auto bc) {
+        constexpr int r0 = kSynPlan<BG, ROWS>.r0[decltype(bc)::value];
+        constexpr int r1 = kSynPlan<BG, ROWS>.r1[decltype(bc)::value];
+        constexpr int NE = syn_slot<BG, ROWS>(r0, r1, 0);
+        T a[NE > 0 ? NE : 1];
+        sfor<r0, r1>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr ((ROWS >> i) & 1u)
+                sfor<0, P::RS[i + 1] - P::RS[i]>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (P::COL[P::RS[i] + k] < P::KC) a[syn_slot<BG, ROWS>(r0, i, k)] = core(ic, kc);
+                });
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        sfor<r0, r1>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr ((ROWS >> i) & 1u) {
+                bool par = false;
+                if constexpr (i >= 4) par = ext(ic);
+                sfor<0, P::RS[i + 1] - P::RS[i]>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    if constexpr (P::COL[P::RS[i] + k] < P::KC) {
+                        const T v = a[syn_slot<BG, ROWS>(r0, i, k)];
+                        par ^= STRICT ? v < T(0) : v <= T(0);
+                    }
+                });
+                fail |= par;
+            }
+        });
+    });
+    return fail;
+}
+template <int BG>
+constexpr uint64_t all_rows() { return BGT<BG>::MB >= 64 ? ~0ull : (1ull << BGT<BG>::MB) - 1; }
+
 // ---- ck through LDS (both decoders).  The decisions of a workgroup's slots are staged in LDS in
 // output order (byte j*Zc + z of slot s at s*SS, SS = Nf*Zc rounded up to 16) once the decoding is
 // over, then written as 16-B pieces of whole rows: every 128-B line of ck is written once and in
@@ -609,22 +688,12 @@ __device__ __forceinline__ void dec_body(
             const bool cand = active && flagA[cl] == 0;
             if (block_any(cand)) {
                 if (cand) {
-                    bool sf = false;
-                    sfor<0, MB>([&](auto ic) {
-                        constexpr int i = decltype(ic)::value;
-                        constexpr int e0 = P::RS[i];
-                        constexpr int d = P::RS[i + 1] - e0;
-                        bool par = false;
-                        sfor<0, d>([&](auto kc) {
-                            constexpr int k = decltype(kc)::value;
-                            constexpr int j = P::COL[e0 + k];
-                            if constexpr (j < KC)
-                                par ^= at(j * CS * TS + rot(shift_of<BG>(ziv, e0 + k))) < T(0);
-                            else
-                                par ^= (bool)((hdx >> (i - 4)) & 1u);
-                        });
-                        sf |= par;
-                    });
+                    const bool sf = syndrome_fails<BG, all_rows<BG>(), true, T>(
+                        [&](auto ic, auto kc) -> T {
+                            constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
+                            return at(P::COL[e] * CS * TS + rot(shift_of<BG>(ziv, e)));
+                        },
+                        [&](auto ic) -> bool { return (hdx >> (decltype(ic)::value - 4)) & 1u; });
                     if (sf) flagB[cl] = 1;
                 }
                 lds_barrier();
@@ -648,33 +717,28 @@ __device__ __forceinline__ void dec_body(
     zv = z;
     asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
     if (active) {
-        // every extension LLR is requested before the pass uses any: one round trip, not one per
-        // row (the scheduler serialised them under the pass's register pressure: ~30 us per WG)
-        T vx[MB - 4];
-#pragma unroll
-        for (int i4 = 0; i4 < MB - 4; ++i4) vx[i4] = llrx(i4);
-        __builtin_amdgcn_sched_barrier(0);
-        bool fail = false;
+        // extension decisions first, their LLRs requested in batches of 14 before any is used (one
+        // load per row made the scheduler serialise them; all 42 at once spill), so the row state
+        // is dead before the syndrome pass
         uint64_t ox = 0;
-        sfor<0, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i];
-            constexpr int d = P::RS[i + 1] - e0;
-            bool par = false;
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int j = P::COL[e0 + k];
-                T a;
-                if constexpr (j < KC) {
-                    a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
-                } else {
-                    a = vx[i - 4] + rfinal(ic, d, k);
-                    ox |= (uint64_t)(a <= T(0)) << (i - 4);
-                }
-                par ^= (a <= T(0));
+        constexpr int XB = 14, NX = MB - 4;
+        sfor<0, (NX + XB - 1) / XB>([&](auto bc) {
+            constexpr int x0 = decltype(bc)::value * XB, x1 = x0 + XB < NX ? x0 + XB : NX;
+            T vx[XB];
+            sfor<x0, x1>([&](auto xc) { vx[decltype(xc)::value - x0] = llrx(decltype(xc)::value); });
+            __builtin_amdgcn_sched_barrier(0);
+            sfor<x0, x1>([&](auto xc) {
+                constexpr int i = decltype(xc)::value + 4;
+                constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+                ox |= (uint64_t)(vx[i - 4 - x0] + rfinal(std::integral_constant<int, i>{}, dl + 1, dl) <= T(0)) << (i - 4);
             });
-            fail |= par;
         });
+        const bool fail = syndrome_fails<BG, all_rows<BG>(), false, T>(
+            [&](auto ic, auto kc) -> T {
+                constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
+                return at(P::COL[e] * CS * TS + rot(shift_of<BG>(zi, e)));
+            },
+            [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
         if (fail) flagA[cl] = 1;
         uint32_t oc = 0;
         for (int j = 0; j < KC; ++j) oc |= (uint32_t)(own(j) <= T(0)) << j;

@@ -632,44 +632,42 @@ __device__ __forceinline__ void flood_body(
     uint32_t oc = 0;          // own core columns (bit j - h*KH): LQ <= 0, or LQ_old < 0 if decided
     uint64_t ox = hdx_keep;   // own extension columns
     if (active) {
-        // the owned rows' extension LLRs are all requested before the pass uses any (one round trip)
-        constexpr int NXMAX = [] {
-            int m = 0;
-            for (int p = 0; p < NP; ++p) m = m > kFloodPlan<BG, T, NP, CS>.nx[p] ? m : kFloodPlan<BG, T, NP, CS>.nx[p];
-            return m;
-        }();
-        T vx[NXMAX > 0 ? NXMAX : 1];
-        per_half([&](auto hc) {
-            constexpr int hh = decltype(hc)::value;
-            sfor<0, kFloodPlan<BG, T, NP, CS>.nx[hh]>([&](auto pc_) {
-                vx[decltype(pc_)::value] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][decltype(pc_)::value]);
-            });
-        });
-        __builtin_amdgcn_sched_barrier(0);
-        bool fail = false;
+        // the owned rows' extension decisions first, their LLRs requested in batches of 8 before any
+        // is used (the row state is dead before the syndrome pass)
         ox = 0;
         per_half([&](auto hc) {
-            sfor<0, MB>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                constexpr int e0 = P::RS[i];
-                constexpr int d = P::RS[i + 1] - e0;
-                if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {
-                    bool par = false;
-                    sfor<0, d>([&](auto kc) {
-                        constexpr int k = decltype(kc)::value;
-                        constexpr int j = P::COL[e0 + k];
-                        T a;
-                        if constexpr (j < KC) {
-                            a = at(j * CS * TS + rot(shift_of<BG>(zi, e0 + k)));
-                        } else {
-                            a = vx[kFloodPlan<BG, T, NP, CS>.xpos[i]] + rfinal(ic, k);
-                            ox |= (uint64_t)(a <= T(0)) << (i - 4);
-                        }
-                        par ^= (a <= T(0));
-                    });
-                    fail |= par;
-                }
+            constexpr int hh = decltype(hc)::value;
+            constexpr int NX = kFloodPlan<BG, T, NP, CS>.nx[hh], XB = 8;
+            sfor<0, (NX + XB - 1) / XB>([&](auto bc) {
+                constexpr int x0 = decltype(bc)::value * XB, x1 = x0 + XB < NX ? x0 + XB : NX;
+                T vx[XB];
+                sfor<x0, x1>([&](auto xc) {
+                    vx[decltype(xc)::value - x0] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][decltype(xc)::value]);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+                sfor<x0, x1>([&](auto xc) {
+                    constexpr int i = kFloodPlan<BG, T, NP, CS>.xlist[hh][decltype(xc)::value];
+                    constexpr int dl = P::RS[i + 1] - P::RS[i] - 1;   // ext column = last edge
+                    ox |= (uint64_t)(vx[decltype(xc)::value - x0] + rfinal(std::integral_constant<int, i>{}, dl) <= T(0))
+                          << (i - 4);
+                });
             });
+        });
+        bool fail = false;
+        per_half([&](auto hc) {
+            constexpr int hh = decltype(hc)::value;
+            constexpr uint64_t rows = [] {
+                uint64_t m = 0;
+                for (int i = 0; i < P::MB; ++i)
+                    if (kFloodPlan<BG, T, NP, CS>.owner[i] == hh) m |= 1ull << i;
+                return m;
+            }();
+            fail = syndrome_fails<BG, rows, false, T>(
+                [&](auto ic, auto kc) -> T {
+                    constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
+                    return at(P::COL[e] * CS * TS + rot(shift_of<BG>(zi, e)));
+                },
+                [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
         });
         if (fail) flagA[cl] = 1;
     }

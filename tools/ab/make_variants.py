@@ -203,27 +203,31 @@ VARIANTS.update({"lay_pre4": (LAYERED, _pre(4)), "lay_pre8": (LAYERED, _pre(8)),
 
 
 # instrumentation (wrong ck rows): thread 0 of every workgroup records the real-time clock (100 MHz)
-# at 6 points — start, after the prologue, after iteration 1, loop exit, after the final syndrome
-# pass, after the ck store — into the first 48 bytes of its first codeblock's ck row
-# (tools/ts_probe.py reads them): where a workgroup's fixed (per-launch, not per-iteration) time goes
-_TS = [
-    ("    const int t = threadIdx.x;\n    if (work) {\n        DecWork w = work[blockIdx.x];",
-     "    const int t = threadIdx.x;\n    uint64_t ts[6];\n    ts[0] = __builtin_amdgcn_s_memrealtime();\n"
-     "    if (work) {\n        DecWork w = work[blockIdx.x];"),
-    ("    bool active = valid;\n    lds_barrier();\n",
-     "    bool active = valid;\n    lds_barrier();\n    ts[1] = __builtin_amdgcn_s_memrealtime();\n"),
-    ("        if (!block_any(active)) break;\n    }\n",
-     "        if (it == 0) ts[2] = __builtin_amdgcn_s_memrealtime();\n        if (!block_any(active)) break;\n    }\n"
-     "    ts[3] = __builtin_amdgcn_s_memrealtime();\n"),
-    ("    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here\n",
-     "    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here\n"
-     "    ts[4] = __builtin_amdgcn_s_memrealtime();\n"),
-    ("        }, slow, t, (int)blockDim.x);\n    }\n}\n",
-     "        }, slow, t, (int)blockDim.x);\n    }\n    __syncthreads();\n    ts[5] = __builtin_amdgcn_s_memrealtime();\n"
-     "    if (t == 0 && !work) {\n        uint64_t* o = (uint64_t*)(ck + (int64_t)((int)blockIdx.x * G) * ldc);\n"
-     "        for (int k = 0; k < 6; ++k) o[k] = ts[k];\n    }\n}\n"),
-]
-VARIANTS.update({"lay_ts": (LAYERED, _TS)})
+# at 7 points — start, after the prologue, after iteration 1, loop exit, after the final syndrome
+# pass, after the ck store, and (slot 6) after the prologue's LLR loads were consumed — into the
+# first 56 bytes of its first codeblock's ck row (tools/ts_probe.py reads them)
+def _ts(flood):
+    rt = "__builtin_amdgcn_s_memrealtime()"
+    final = ("    lds_barrier();   // every LQ / state read is done: LDS below FLAG_B is free from here\n" if flood else
+             "    lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here\n")
+    loads = ("        if constexpr (DEAD)\n            per_half_init(" if flood else
+             "    for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);\n")
+    p = [
+        ("    const int t = threadIdx.x;\n", f"    const int t = threadIdx.x;\n    uint64_t ts[7] = {{}};\n    ts[0] = {rt};\n"),
+        ("    bool active = valid;\n    lds_barrier();\n", f"    bool active = valid;\n    lds_barrier();\n    ts[1] = {rt};\n"),
+        ("        if (!block_any(active)) break;\n    }\n",
+         f"        if (it == 0) ts[2] = {rt};\n        if (!block_any(active)) break;\n    }}\n    ts[3] = {rt};\n"),
+        (final, final + f"    ts[4] = {rt};\n"),
+        (loads, f"    ts[6] = {rt};\n" + loads),
+        ("        }, slow, t, (int)blockDim.x);\n    }\n}\n",
+         f"        }}, slow, t, (int)blockDim.x);\n    }}\n    __syncthreads();\n    ts[5] = {rt};\n"
+         "    if (t == 0 && !work) {\n        uint64_t* o = (uint64_t*)(ck + (int64_t)((int)blockIdx.x * G) * ldc);\n"
+         "        for (int k = 0; k < 7; ++k) o[k] = ts[k];\n    }\n}\n"),
+    ]
+    return p
+
+
+VARIANTS.update({"lay_ts": (LAYERED, _ts(False)), "flood_ts": (FLOOD, _ts(True))})
 
 
 def make(name):
