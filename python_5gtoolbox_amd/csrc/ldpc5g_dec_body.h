@@ -203,11 +203,17 @@ constexpr int syn_slot(int r0, int i, int k) {
     return n;
 }
 // true when some row of ROWS fails: parity over its core edges of (core(ic, kc) < 0) [STRICT] or
-// (<= 0), XOR ext(ic) (the decision of the row's extension edge; rows >= 4 only)
-template <int BG, uint64_t ROWS, bool STRICT, typename T, typename Core, typename Ext>
+// (<= 0), XOR ext(ic) (the decision of the row's extension edge; rows >= 4 only; called without side
+// effects).  VPAR: the parity is the sign bit of the XOR of the values' (high) words, all VALU (the
+// compare + lane-mask XOR per edge ran on the CU's one scalar unit for all 12 waves), exact unless
+// a value is +-0 — a min |v| per row detects that, and then (rare; one wave-uniform branch for the
+// whole pass) the compare pass decides those lanes.  !VPAR: the compare pass (also the layered
+// stop rule inside the iteration loop, where the VALU form's registers spilled).
+template <int BG, uint64_t ROWS, bool STRICT, typename T, bool VPAR = false, typename Core, typename Ext>
 __device__ __forceinline__ bool syndrome_fails(Core&& core, Ext&& ext) {
     using P = BGT<BG>;
-    bool fail = false;
+    uint32_t fails = 0;
+    bool zany = false;
     sfor<0, kSynPlan<BG, ROWS>.n>([&](auto bc) {
         constexpr int r0 = kSynPlan<BG, ROWS>.r0[decltype(bc)::value];
         constexpr int r1 = kSynPlan<BG, ROWS>.r1[decltype(bc)::value];
@@ -222,23 +228,44 @@ __device__ __forceinline__ bool syndrome_fails(Core&& core, Ext&& ext) {
                 });
         });
         __builtin_amdgcn_sched_barrier(0);
+        T zm = FT<T>::inf();
         sfor<r0, r1>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             if constexpr ((ROWS >> i) & 1u) {
-                bool par = false;
-                if constexpr (i >= 4) par = ext(ic);
-                sfor<0, P::RS[i + 1] - P::RS[i]>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    if constexpr (P::COL[P::RS[i] + k] < P::KC) {
-                        const T v = a[syn_slot<BG, ROWS>(r0, i, k)];
-                        par ^= STRICT ? v < T(0) : v <= T(0);
-                    }
-                });
-                fail |= par;
+                constexpr int n0 = syn_slot<BG, ROWS>(r0, i, 0), n1 = syn_slot<BG, ROWS>(r0, i + 1, 0);
+                if constexpr (VPAR) {
+                    uint32_t sx = 0;
+                    sfor<n0, n1>([&](auto nc) {
+                        constexpr int n = decltype(nc)::value;
+                        if constexpr ((n - n0) % 2 == 1)
+                            sx = __builtin_amdgcn_bitop3_b32(sx, FT<T>::sbits(a[n - 1]), FT<T>::sbits(a[n]), 0x96);
+                        else if constexpr (n == n1 - 1)
+                            sx ^= FT<T>::sbits(a[n]);
+                        zm = fmin(zm, fabs(a[n]));
+                    });
+                    uint32_t par = sx >> 31;
+                    if constexpr (i >= 4) par ^= (uint32_t)ext(ic);
+                    fails |= par;
+                } else {
+                    bool pb = false;
+                    if constexpr (i >= 4) pb = ext(ic);
+                    sfor<n0, n1>([&](auto nc) {
+                        const T v = a[decltype(nc)::value];
+                        pb ^= STRICT ? v < T(0) : v <= T(0);
+                    });
+                    fails |= (uint32_t)pb;
+                }
             }
         });
+        if constexpr (VPAR) zany |= zm == T(0);
     });
-    return fail;
+    if constexpr (VPAR) {
+        if (__builtin_amdgcn_ballot_w64(zany) != 0) {   // some lane saw a +-0: compare pass
+            const bool slow = syndrome_fails<BG, ROWS, STRICT, T, false>(core, ext);
+            if (zany) fails = slow;
+        }
+    }
+    return fails != 0;
 }
 template <int BG>
 constexpr uint64_t all_rows() { return BGT<BG>::MB >= 64 ? ~0ull : (1ull << BGT<BG>::MB) - 1; }
@@ -424,23 +451,27 @@ __device__ __forceinline__ void dec_body(
     if (valid) {
         // all Nf - pc loads are issued before any is used: one HBM round trip per workgroup
         // (a conditional load per punctured column made 26 + 6 dependent round trips, ~40 us)
+        // (the extension LLRs only for DEAD, for the live-row mask: otherwise their initial hard
+        // decisions are taken in iteration 0 from the loads the row loop issues anyway)
         T vc[KC], vx[MB - 4];
 #pragma unroll
         for (int j = 0; j < KC; ++j) vc[j] = lrow[(j < pc ? 0 : j - pc) * Zc + z];
+        if constexpr (DEAD)
 #pragma unroll
-        for (int i4 = 0; i4 < MB - 4; ++i4) vx[i4] = lrow[(KB + 4 + i4 - pc) * Zc + z];
+            for (int i4 = 0; i4 < MB - 4; ++i4) vx[i4] = lrow[(KB + 4 + i4 - pc) * Zc + z];
 #pragma unroll
         for (int j = 0; j < KC; ++j) {
             const T v = j < pc ? T(0) : vc[j];   // punctured columns: LLR 0 (:43)
             own(j) = v;
             hdc_prev |= (uint32_t)(v < T(0)) << j;
         }
+        if constexpr (DEAD)
 #pragma unroll
-        for (int i4 = 0; i4 < MB - 4; ++i4) {
-            const T v = vx[i4];
-            hdx_prev |= (uint64_t)(v < T(0)) << i4;
-            nzx |= (uint64_t)(FT<T>::bits(v) != 0) << i4;
-        }
+            for (int i4 = 0; i4 < MB - 4; ++i4) {
+                const T v = vx[i4];
+                hdx_prev |= (uint64_t)(v < T(0)) << i4;
+                nzx |= (uint64_t)(FT<T>::bits(v) != 0) << i4;
+            }
     }
     for (int w = 0; w < 2 * NLR; ++w) at(ST_B + w * CS * TS + tzb) = T(0);
     if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
@@ -534,6 +565,8 @@ __device__ __forceinline__ void dec_body(
                     q[k] = at(j * CS * TS + rb[k]) - rold;
                 } else {
                     q[k] = xl;   // degree-1 column: q is the channel LLR itself
+                    if constexpr (!DEAD)   // initial hard decision of the ext column (see prologue)
+                        if (it == 0) hdx_prev |= (uint64_t)(xl < T(0)) << (i - 4);
                 }
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
                 const T aq = fabs(q[k]);
@@ -688,7 +721,7 @@ __device__ __forceinline__ void dec_body(
             const bool cand = active && flagA[cl] == 0;
             if (block_any(cand)) {
                 if (cand) {
-                    const bool sf = syndrome_fails<BG, all_rows<BG>(), true, T>(
+                    const bool sf = syndrome_fails<BG, all_rows<BG>(), true, T, false>(
                         [&](auto ic, auto kc) -> T {
                             constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
                             return at(P::COL[e] * CS * TS + rot(shift_of<BG>(ziv, e)));
@@ -714,6 +747,14 @@ __device__ __forceinline__ void dec_body(
         return decomp_l(getA(ic), getB(ic), pk, pk >> 24, d, k);
     };
     // ---- iterations exhausted: ck = (APP <= 0), status = syndrome == 0 (:133-143)
+    // rotated address for the final syndrome pass, multiplied on the VALU (v_mul_u32_u24 with an
+    // opaque VGPR stride): the scalar unit is shared by the workgroup's 12 waves
+    uint32_t GTv = GT;
+    asm volatile("" : "+v"(GTv));
+    auto rot_v = [&](int sft) -> int {
+        const uint32_t S = __umul24((uint32_t)sft, GTv);
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
     zv = z;
     asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
     if (active) {
@@ -736,7 +777,7 @@ __device__ __forceinline__ void dec_body(
         const bool fail = syndrome_fails<BG, all_rows<BG>(), false, T>(
             [&](auto ic, auto kc) -> T {
                 constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
-                return at(P::COL[e] * CS * TS + rot(shift_of<BG>(zi, e)));
+                return at(P::COL[e] * CS * TS + rot_v(shift_of<BG>(zi, e)));
             },
             [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
         if (fail) flagA[cl] = 1;

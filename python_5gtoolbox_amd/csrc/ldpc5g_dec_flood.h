@@ -361,6 +361,14 @@ __device__ __forceinline__ void flood_body(
         const uint32_t S = (uint32_t)sft * GT;
         return (int)min((uint32_t)tzb + S, tzbw + S);
     };
+    // the same on the VALU (v_mul_u32_u24 with an opaque VGPR stride) for the final syndrome pass:
+    // the scalar unit is shared by the workgroup's 12 waves
+    uint32_t GTv = GT;
+    asm volatile("" : "+v"(GTv));
+    auto rot_v = [&](int sft) -> int {
+        const uint32_t S = __umul24((uint32_t)sft, GTv);
+        return (int)min((uint32_t)tzb + S, tzbw + S);
+    };
     // f(integral_constant<half>): each half's rows form one basic block, so the scheduler can
     // overlap a row's LDS reads with the previous row's arithmetic
     auto per_half = [&](auto&& f) {
@@ -665,7 +673,7 @@ __device__ __forceinline__ void flood_body(
             fail = syndrome_fails<BG, rows, false, T>(
                 [&](auto ic, auto kc) -> T {
                     constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
-                    return at(P::COL[e] * CS * TS + rot(shift_of<BG>(zi, e)));
+                    return at(P::COL[e] * CS * TS + rot_v(shift_of<BG>(zi, e)));
                 },
                 [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
         });
