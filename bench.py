@@ -14,6 +14,7 @@ the K steps, max over ranks.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -236,6 +237,66 @@ def bench_config1(rank, n=300):
             "encode_us_per_call": round((t1 - t0) / n * 1e6, 1),
             "decode_us_per_call": round((t2 - t1) / n * 1e6, 1), "calls": n,
             "reference_cpu_ms_per_call": {"encode": "1.2-2.2", "decode": "30-57"}}
+
+
+def bench_dlsch_caller(rank, reps=5):
+    """Per-codeblock drop-in latency in the reference's own caller shape: DLSCHDecode's loop over
+    the C codeblocks of one TB (/root/reference/py5gphy/nr_pdsch/nr_dlsch_decode.py:62-103: rate
+    recovery, nr_decode_ldpc, CB CRC per codeblock, then the TB CRC) restated here over this
+    package's drop-ins — what a user gets who swaps only the py5gphy.ldpc / crc modules ("codec-only
+    swap") — beside the module swap, where DLSCHDecode itself is the drop-in that runs the whole TB
+    through the GPU chain in one call.  TB: A = 193,728 bits, C = 23 BG1 Zc=384 codeblocks, 256QAM,
+    2 layers, R = 700/1024, G = 278,016, float64 flooding NMS alpha=0.75 L=8, 30 dB BPSK LLRs."""
+    import numpy as np
+    from python_5gtoolbox_amd import crc, ldpc_info, nr_dlsch, nr_dlsch_decode, nr_ldpc_decode, \
+        nr_ldpc_ratematch, nr_ldpc_raterecover
+    A, Qm, R, NL, rv, LBRM, G = 193728, 8, 700, 2, 0, 1081512, 278016
+    dec = {"L": 8, "algo": "min-sum", "alpha": 0.75, "beta": 0.0}
+    rng = np.random.default_rng(11 + rank)
+    tb = rng.integers(0, 2, A).astype(np.int8)
+    g = nr_dlsch.DLSCHEncode(tb, A, Qm, R, NL, rv, LBRM, G)
+    llr = (1 - 2 * g.astype(np.float64)) * 20.0 + rng.normal(0, 0.5, G)
+
+    def codec_only():   # nr_dlsch_decode.py:16-106 with the codec modules swapped
+        B, poly = A + 24, "24A"
+        bgn = 1
+        C, cbz, Lc, F, K, Zc = ldpc_info.get_cbs_info(B, bgn)
+        K_apo = cbz + Lc
+        N = 66 * Zc
+        Ncb = min(N, math.floor(LBRM / (C * 2 / 3)))
+        k0 = nr_ldpc_ratematch.get_k0(Ncb, bgn, rv, Zc)
+        Er = nr_ldpc_ratematch.get_Er_ldpc(G, C, Qm, NL)
+        tbb = np.zeros(B)
+        to = go = 0
+        for c in range(C):
+            E = Er[c]
+            dn = nr_ldpc_raterecover.raterecover_ldpc(llr[go:go + E], Ncb, N, k0, Qm, Zc, K_apo, K)
+            go += E
+            blkandcrc, ck, status = nr_ldpc_decode.nr_decode_ldpc(dn, Zc, bgn, dec["L"], dec["algo"],
+                                                                  dec["alpha"], dec["beta"])
+            cbblk, err = crc.nr_crc_decode(blkandcrc[0:K_apo], "24B")
+            tbb[to:to + cbz] = cbblk
+            to += cbz
+        blk, e = crc.nr_crc_decode(tbb.astype(np.int8), poly)
+        return e == 0, blk
+
+    def module_swap():
+        ok, blk, _ = nr_dlsch_decode.DLSCHDecode(llr, A, Qm, R, NL, rv, LBRM, dec)
+        return ok, blk
+
+    res = {}
+    for name, fn in (("codec_only_swap", codec_only), ("module_swap", module_swap)):
+        ok, blk = fn()
+        res[name + "_tb_bits_match"] = bool(ok and np.array_equal(np.asarray(blk, np.int8), tb))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        res[name + "_ms_per_tb"] = round((time.perf_counter() - t0) / reps * 1e3, 2)
+    return {"workload": "one 23-codeblock DL-SCH TB (BG1 Zc=384) through DLSCHDecode's per-codeblock "
+                        "loop (nr_dlsch_decode.py:62-103) with only the codec swapped, vs DLSCHDecode "
+                        "swapped (whole TB on the GPU in one call); float64 flooding, host arrays in/out",
+            **res, "codeblocks_per_tb": 23,
+            "codec_only_ms_per_codeblock": round(res["codec_only_swap_ms_per_tb"] / 23, 3)}
 
 
 def bench_config4(torch, dist, world, dev, rank, steps):
@@ -531,6 +592,7 @@ def main():
             "achieved_GBps": round(ach_h, 1), "frac": round(ach_h / HBM_PEAK_GBS, 4)}
         del ckh, dnh
         ex["config1_per_codeblock"] = bench_config1(rank)
+        ex["dlsch_caller_shape"] = bench_dlsch_caller(rank)
         tm = {}
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded
         if world == 1 or dist.get_backend() == "nccl":   # gloo cannot gather device tensors
