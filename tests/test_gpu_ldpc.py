@@ -427,3 +427,33 @@ def test_mixed_batch_rate_matched_vs_oracle(torch, schedule):
             assert np.array_equal(ck[co:co + nf], ref[0][r]), (bg, Zc, r)
             assert st[k] == ref[1][r] and it[k] == ref[2][r], (bg, Zc, r)
             k += 1
+
+
+@pytest.mark.parametrize("bg,Zc", [(2, 13), (1, 15), (1, 9), (2, 6)])
+@pytest.mark.parametrize("schedule,dtype", [("layered", np.float32), ("flooding", np.float32),
+                                            ("flooding", np.float64)])
+def test_decode_ck_store_unaligned_rows(torch, dec, bg, Zc, schedule, dtype):
+    """The staged ck store (ck_store_staged): rows whose length Nf*Zc is not a multiple of 16 and
+    rows in a padded, odd-offset view of a wider buffer take the byte path; slots of several
+    workgroups incl. a batch tail.  ck / status / iters == oracle, padding bytes untouched."""
+    rng = np.random.default_rng(Zc * 10 + bg)
+    K, N, Nf = ((22, 66, 68) if bg == 1 else (10, 50, 52))
+    B = 100
+    ck0 = rng.integers(0, 2, (B, K * Zc)).astype(np.int8)
+    dn = O.encode(ck0, bg)
+    snr = np.repeat([-1.0, 1.0, 3.0, 6.0], B // 4)[:, None]
+    llr = (2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
+           10 ** (-snr / 10)).astype(dtype)
+    ref = (O.decode_layered(llr, Zc, bg, 6, 0.75, 0.0) if schedule == "layered"
+           else O.decode_flooding(llr, Zc, bg, 6, 0.75, 0.0, dtype))
+    x = torch.from_numpy(llr).cuda()
+    for pad, off in ((0, 0), (21, 3)):
+        wide = torch.full((B, Nf * Zc + pad + off), 0x55, dtype=torch.int8, device="cuda")
+        ckv = wide[:, off:off + Nf * Zc]
+        st = torch.empty((B,), dtype=torch.uint8, device="cuda")
+        it = torch.empty((B,), dtype=torch.int32, device="cuda")
+        dec.nr_decode_ldpc_batch(x, Zc, bg, 6, "min-sum", 0.75, 0.0, schedule, out=(ckv, st, it))
+        w = wide.cpu().numpy()
+        assert np.array_equal(w[:, off:off + Nf * Zc], ref[0]), (pad, off)
+        assert np.array_equal(st.cpu().numpy(), ref[1]) and np.array_equal(it.cpu().numpy(), ref[2])
+        assert (w[:, :off] == 0x55).all() and (w[:, off + Nf * Zc:] == 0x55).all(), (pad, off)
