@@ -7,6 +7,8 @@ import ctypes
 import os
 import threading
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LDPC5G_LIB") or os.path.join(HERE, "libldpc5g.so")
 
@@ -204,3 +206,31 @@ def staging(key, make):
     if b is None:
         b = d[key] = make()
     return b
+
+
+def to_device(a, key):
+    """numpy array -> device tensor through a per-thread cached pinned buffer (the drop-ins'
+    host inputs; pageable copies measured milliseconds per call).  The device buffer is reused by
+    the next call with the same key and shape: callers synchronise (to_host) before returning."""
+    t = torch()
+    a = np.ascontiguousarray(a)
+    dev = t.cuda.current_device()
+    tdt = t.from_numpy(a[:0] if a.ndim else a.reshape(1)[:0]).dtype
+
+    def make():
+        return (t.empty(a.shape, dtype=tdt, pin_memory=True), t.empty(a.shape, dtype=tdt, device=dev))
+    hin, din = staging((key, "in", dev, a.shape, a.dtype.str), make)
+    hin.numpy()[...] = a
+    din.copy_(hin, non_blocking=True)
+    return din
+
+
+def to_host(x, key):
+    """device tensor -> numpy copy through a per-thread cached pinned buffer; synchronises."""
+    t = torch()
+    dev = x.device.index if x.device.index is not None else t.cuda.current_device()
+    hout = staging((key, "out", dev, tuple(x.shape), str(x.dtype)),
+                   lambda: t.empty(tuple(x.shape), dtype=x.dtype, pin_memory=True))
+    hout.copy_(x, non_blocking=True)
+    t.cuda.current_stream().synchronize()
+    return hout.numpy().copy()

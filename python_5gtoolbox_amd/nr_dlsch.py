@@ -18,8 +18,8 @@ def DLSCHEncode(trblk, TBSize, Qm, coderateby1024, num_of_layers, rv, TBS_LBRM, 
     assert (not np.any(trblk < 0)) and (not np.any(trblk > 1))   # crc.py:18-20
     t = _lib.require_gpu()
     cfg = sch_config(TBSize, Qm, coderateby1024, num_of_layers, rv, TBS_LBRM, G)
-    x = t.from_numpy(np.ascontiguousarray(trblk, dtype=np.int8).reshape(1, -1)).cuda()
-    g = sch_encode_batch(x, cfg)[0].cpu().numpy()
+    x = _lib.to_device(np.asarray(trblk, dtype=np.int8).reshape(1, -1), "dlsch_enc")
+    g = _lib.to_host(sch_encode_batch(x, cfg)[0], "dlsch_enc")
     out = np.zeros(G, "i1")
     out[:g.size] = g
     return out

@@ -17,9 +17,9 @@ def ULSCH_Crc_CodeBlockSegment(trblk, TBSize, coderateby1024):
     t = _lib.require_gpu()
     # Qm / NL / rv / G do not influence segmentation; any valid values do
     cfg = sch_config(TBSize, 2, coderateby1024, 1, 0, 0, 2)
-    x = t.from_numpy(np.ascontiguousarray(trblk, dtype=np.int8).reshape(1, -1)).cuda()
+    x = _lib.to_device(np.asarray(trblk, dtype=np.int8).reshape(1, -1), "ulsch_seg")
     ck, _ = sch_segment_batch(x, cfg)
-    return ck.cpu().numpy(), cfg.Zc, cfg.bgn
+    return _lib.to_host(ck, "ulsch_seg"), cfg.Zc, cfg.bgn
 
 
 def ULSCH_encoding_ratematch(cbs, Zc, bgn, Qm, G_ULSCH, num_of_layers, rv):
@@ -32,8 +32,8 @@ def ULSCH_encoding_ratematch(cbs, Zc, bgn, Qm, G_ULSCH, num_of_layers, rv):
     fill = np.nonzero(cbs[0] == -1)[0]
     K_apo = int(fill[0]) if fill.size else K
     cfg = cfg_from_codeblocks(C, K, K_apo, Zc, bgn, Qm, G_ULSCH, num_of_layers, rv)
-    x = t.from_numpy(np.ascontiguousarray(cbs, dtype=np.int8)).cuda()
-    g = sch_ratematch_batch(x, cfg, 1)[0].cpu().numpy()
+    x = _lib.to_device(np.asarray(cbs, dtype=np.int8), "ulsch_rm")
+    g = _lib.to_host(sch_ratematch_batch(x, cfg, 1)[0], "ulsch_rm")
     tail = cbs[:, 2 * Zc:]
     tail[tail == -1] = 0
     out = np.zeros(G_ULSCH, "i1")

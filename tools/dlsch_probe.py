@@ -41,3 +41,26 @@ print("sch_decode_batch (device, sync) ms", ms)
 print("D2H llr_dn ms", t(lambda: r.llr_dn.cpu().numpy())[0])
 print("D2H tbblk+ok ms", t(lambda: (r.tbblk[0, :A].cpu().numpy(), r.tb_ok.cpu().numpy()))[0])
 print("mean iterations", r.iters.float().mean().item())
+
+from python_5gtoolbox_amd import _lib  # noqa: E402
+from python_5gtoolbox_amd.sch import SchWorkspace  # noqa: E402
+
+
+def steps():
+    tt = [time.perf_counter()]
+    t_ = _lib.require_gpu(); tt.append(time.perf_counter())
+    ll = np.ascontiguousarray(np.asarray(llr, np.float64).reshape(1, -1)); tt.append(time.perf_counter())
+    xx = t_.from_numpy(ll).cuda(); tt.append(time.perf_counter())
+    ws = SchWorkspace(cfg, 1, xx.device); tt.append(time.perf_counter())
+    rr = sch_decode_batch(xx, cfg, 8, "min-sum", 0.75, 0.0, "flooding", None, torch.float64, ws); tt.append(time.perf_counter())
+    ok = bool(rr.tb_ok.cpu().numpy()[0]); tt.append(time.perf_counter())
+    blk = rr.tbblk[0, :cfg.A].cpu().numpy().astype("i1"); tt.append(time.perf_counter())
+    new = rr.llr_dn.cpu().numpy().astype(np.float64); tt.append(time.perf_counter())
+    return np.diff(tt) * 1e3
+
+
+for _ in range(3):
+    steps()
+acc = np.mean([steps() for _ in range(10)], axis=0)
+print("require_gpu, asarray, H2D, workspace, decode(async), tb_ok D2H(sync), tbblk D2H, llr_dn D2H (ms):",
+      np.round(acc, 3))
