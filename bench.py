@@ -8,9 +8,13 @@ The headline runs at snr -3 dB, where no codeblock converges, so every step does
 iterations plus the final syndrome pass (worst case); `early_exit` repeats it at 1 dB.
 Synthetic data: random info bits -> GPU encoder -> BPSK + AWGN (torch RNG) — no datasets.
 
-Multi-GPU: one process per GPU (torch.distributed.run), each decodes its own 4096-codeblock
-shard (weak scaling, no collective on the data path); timing = barrier + synchronize around
-the K steps, max over ranks.  Rank 0 prints ONE JSON line.
+`reference_precision` repeats config 3 in the reference's own arithmetic and schedule (float64
+flooding, bit-identical to nr_decode_ldpc) with its own roofline and same-algorithm CPU baseline.
+
+Multi-GPU: one process per GPU (torch.distributed.run, or `--gpus N` alone, which starts the N
+rank processes itself), each decodes its own 4096-codeblock shard (weak scaling, no collective on
+the data path); timing = barrier + synchronize around the K steps, max over ranks.  Rank 0 prints
+ONE JSON line.
 """
 import argparse
 import json
@@ -116,6 +120,11 @@ def parse():
                          "multi-rank control flow with several ranks on one GPU)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary measurements (early exit, flooding, encoder)")
+    ap.add_argument("--no-reference", action="store_true",
+                    help="skip the float64 flooding (reference-precision) config-3 line")
+    ap.add_argument("--roctx-region", default="headline", choices=["headline", "reference"],
+                    help="timed region bracketed by roctxProfilerResume/Pause when LDPC5G_ROCTX=1 "
+                         "(rocprofv3 --selected-regions)")
     return ap.parse_args()
 
 
@@ -131,9 +140,25 @@ def make_llr(torch, enc, B, snr_db, seed, dev):
     return ck, dn, llr
 
 
-def timed(torch, dist, world, fn, steps, warmup):
+_ROCTX = []
+
+
+def roctx_region(on):
+    """With LDPC5G_ROCTX=1 (set by tools/gpu_round.sh for `rocprofv3 --selected-regions`), resume /
+    pause the profiler around a timed region, so the committed kernel statistics hold exactly the
+    timed launches (no warmup launches in the average)."""
+    if os.environ.get("LDPC5G_ROCTX") != "1":
+        return
+    if not _ROCTX:
+        import ctypes
+        _ROCTX.append(ctypes.CDLL("librocprofiler-sdk-roctx.so"))
+    (_ROCTX[0].roctxProfilerResume if on else _ROCTX[0].roctxProfilerPause)(0)
+
+
+def timed(torch, dist, world, fn, steps, warmup, region=False):
     """warmup, then exactly `steps` calls bracketed by barrier + synchronize; returns
-    (max-over-ranks wall seconds, this rank's event-timed seconds)."""
+    (max-over-ranks wall seconds, this rank's event-timed seconds).  region: the profiler's
+    selected region (roctx_region) is exactly these `steps` launches."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -142,12 +167,16 @@ def timed(torch, dist, world, fn, steps, warmup):
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    if region:
+        roctx_region(True)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(steps):
         fn()
     e1.record()
     torch.cuda.synchronize()
+    if region:
+        roctx_region(False)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -162,7 +191,8 @@ def timed(torch, dist, world, fn, steps, warmup):
 
 def _cpu_worker(job):
     """One host process of the CPU baseline: the oracle (numpy) decoding 8-codeblock batches of
-    the headline workload until `seconds` have passed."""
+    the headline workload until `seconds` have passed.  schedule "flooding64" is the reference's
+    own algorithm and arithmetic (float64 flooding, nr_ldpc_decode.py:51-143)."""
     seconds, schedule, alpha, L, seed = job
     import numpy as np
     from oracle import ldpc_oracle as O
@@ -170,8 +200,13 @@ def _cpu_worker(job):
     n = 8
     ck = rng.integers(0, 2, (n, K_INFO)).astype(np.int8)
     llr = O.bpsk_awgn_llr(O.encode(ck, BG), -3.0, rng).astype(np.float32)
-    fn = (lambda: O.decode_layered(llr, ZC, BG, L, alpha, 0.0)) if schedule == "layered" else \
-        (lambda: O.decode_flooding(llr, ZC, BG, L, alpha, 0.0, np.float32))
+    if schedule == "layered":
+        fn = lambda: O.decode_layered(llr, ZC, BG, L, alpha, 0.0)   # noqa: E731
+    elif schedule == "flooding64":
+        llr64 = llr.astype(np.float64)
+        fn = lambda: O.decode_flooding(llr64, ZC, BG, L, alpha, 0.0, np.float64)   # noqa: E731
+    else:
+        fn = lambda: O.decode_flooding(llr, ZC, BG, L, alpha, 0.0, np.float32)   # noqa: E731
     done, t0 = 0, time.perf_counter()
     while True:
         fn()
@@ -201,9 +236,11 @@ def cpu_baseline(seconds, schedule, alpha, L, procs):
             cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
     except (OSError, StopIteration):
         pass
+    what = {"layered": "layered float32", "flooding": "flooding float32",
+            "flooding64": "flooding float64 (the reference's algorithm and arithmetic)"}[schedule]
     return {"value": round(done / el, 3), "unit": "codeblocks/s", "cores": procs, "kind": "port",
             "sample": f"{done} BG1 Zc=384 codeblocks (8 per call) over {procs} processes, "
-                      f"{schedule} NMS alpha={alpha} L={L}, snr -3 dB (all iterations), "
+                      f"{what} NMS alpha={alpha} L={L}, snr -3 dB (all iterations), "
                       f"oracle/ldpc_oracle.py numpy, {el:.1f} s; host {cpu}, "
                       f"os.cpu_count()={os.cpu_count()}",
             "reference_measured_in_build_container": {
@@ -420,13 +457,109 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
                        if tm else None)}
 
 
+def bench_reference_precision(torch, dist, world, llr, out, args, cpu64):
+    """BASELINE config 3 at the reference's precision: float64 flooding NMS, bit-identical to
+    nr_decode_ldpc (/root/reference/py5gphy/ldpc/nr_ldpc_decode.py:51-143) — what the drop-in
+    nr_decode_ldpc / DLSCHDecode / ULSCH_decoding run.  Same LLRs (widened to float64), same
+    timing contract as the headline (warmup, barrier + synchronize, max over ranks), launch time
+    from HIP events on the launch stream."""
+    B = llr.shape[0]
+    llr64 = llr.double()
+
+    def step():
+        D = sys.modules["python_5gtoolbox_amd.nr_ldpc_decode"]
+        D.nr_decode_ldpc_batch(llr64, ZC, BG, args.L, "min-sum", args.alpha, 0.0, "flooding", out=out)
+    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup,
+                     region=args.roctx_region == "reference")
+    iters = out[2].float().mean().item()
+    launch_s = ev / args.steps
+    edge_rate = B * EDGES * iters / launch_s
+    lane = edge_rate * ALG_OPS_PER_EDGE / 1e12
+    value = B * world * args.steps / wall
+    traffic = pmc_traffic(DEC64_KERNEL) if B == 4096 else None
+    alg_bytes = B * DEC64_BYTES_PER_CB
+    del llr64
+    return {
+        "what": "BASELINE config 3 at the reference's precision and schedule: float64 flooding NMS "
+                "alpha=%g L=%d, bit-identical to py5gphy nr_decode_ldpc (ck and status, 193 reference "
+                "goldens)" % (args.alpha, args.L),
+        "value": round(value, 1), "unit": "codeblocks/s", "dtype": "f64", "schedule": "flooding",
+        "ms_per_step": round(wall / args.steps * 1e3, 4), "launch_ms": round(launch_s * 1e3, 4),
+        "steps": args.steps, "warmup": args.warmup,
+        "info_gbit_s": round(value * K_INFO / 1e9, 3), "mean_iterations": round(iters, 3),
+        "converged": int(out[1].sum().item()),
+        "roofline": {"bound": "valu", "achieved": round(lane, 3),
+                     "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
+                     "frac": round(lane / VALU_PEAK_TLANE, 4),
+                     "f64_issue_ceiling": round(VALU_PEAK_TLANE / 2, 1),
+                     "frac_of_f64_ceiling": round(lane / (VALU_PEAK_TLANE / 2), 4),
+                     "traffic": traffic, "algorithmic_bytes": alg_bytes,
+                     "traffic_over_algorithmic": round(traffic / alg_bytes, 3) if traffic else None,
+                     "kernel": DEC64_KERNEL,
+                     "hbm_achieved_GBps": round(alg_bytes / launch_s / 1e9, 2),
+                     "hbm_frac": round(alg_bytes / launch_s / 1e9 / HBM_PEAK_GBS, 5),
+                     "algorithmic": f"{ALG_OPS_PER_EDGE} lane-ops per edge-update x 121,344 edges x "
+                                    f"mean iterations per codeblock; bytes {DEC64_BYTES_PER_CB} per "
+                                    f"codeblock (f64 LLR in, ck, status, iters)",
+                     "note": "two ceilings: the full-rate lane peak (78.6 T) and the float64 issue "
+                             "ceiling (39.3 T: v_add/min/max/cmp_f64 issue at half rate on gfx950, "
+                             "profiles/r02/r02o_valu_rates_f64.txt); traffic = FETCH_SIZE + "
+                             "WRITE_SIZE per launch, profiles/pmc_latest.json"},
+        "valu": valu_block(edge_rate, launch_s, DEC64_KERNEL, B),
+        "cpu_baseline": cpu64,
+    }
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` without an external launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, as
+    torch.distributed.run would) before this process touches the GPU; exit with the first failing
+    rank's code (the other ranks are then stopped by PID)."""
+    import socket
+    import subprocess
+    if args.backend == "nccl":
+        import torch   # device_count() does not initialise the GPU
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {ndev} visible "
+                             f"(--backend gloo rehearses several ranks on one GPU)\n")
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in procs:
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
+        sys.exit(2)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cpu_res = None
+    cpu_res = cpu64 = None
     if rank == 0 and args.cpu_seconds > 0:   # before any GPU initialisation
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
         seconds = args.cpu_seconds
@@ -436,9 +569,13 @@ def main():
         if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
             procs = 1   # a profiler may have initialised the GPU already: no spawned workers
         cpu_res = cpu_baseline(seconds, args.schedule, args.alpha, args.L, procs)
+        cpu64 = cpu_baseline(seconds, "flooding64", args.alpha, args.L, procs)
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > ndev:
+        sys.stderr.write(f"bench.py: {world} ranks but {ndev} GPUs visible\n")
+        sys.exit(2)
     dev = torch.device("cuda", local % max(ndev, 1))   # one rank per GPU (several only to rehearse)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -459,7 +596,8 @@ def main():
         D.nr_decode_ldpc_batch(llr, ZC, BG, args.L, "min-sum", args.alpha, 0.0, args.schedule,
                                out=out)
 
-    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup)
+    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup,
+                     region=args.roctx_region == "headline")
     iters = out[2].float().mean().item()
     conv = int(out[1].sum().item())
     total_cb = B * world * args.steps
@@ -506,6 +644,9 @@ def main():
                              "measured instruction rate is in `valu`"},
         "valu": valu_block(edge_rate, launch_s, DEC_KERNEL[args.schedule], B),
     }
+    if not args.no_reference:
+        res["reference_precision"] = bench_reference_precision(torch, dist, world, llr, out, args,
+                                                               cpu64)
 
     if not args.no_extras:
         ex = {}
@@ -528,34 +669,6 @@ def main():
         ex[f"{other}_f32_snr{args.snr:g}dB"] = {
             "codeblocks_per_s": round(B * world * max(3, args.steps // 2) / w2, 1),
             "mean_iterations": round(out[2].float().mean().item(), 3)}
-        # the reference-parity mode: float64 flooding, bit-identical to nr_decode_ldpc (what the
-        # drop-in per-codeblock API and DLSCHDecode run by default)
-        llr64 = llr.double()
-
-        def step2b():
-            D.nr_decode_ldpc_batch(llr64, ZC, BG, args.L, "min-sum", args.alpha, 0.0, "flooding",
-                                   out=out)
-        n2b = max(3, args.steps // 4)
-        w2b, _ = timed(torch, dist, world, step2b, n2b, 1)
-        f64_launch = w2b / n2b
-        ex[f"flooding_f64_snr{args.snr:g}dB"] = {
-            "codeblocks_per_s": round(B * world * n2b / w2b, 1),
-            "mean_iterations": round(out[2].float().mean().item(), 3),
-            "ms_per_call": round(f64_launch * 1e3, 4),
-            "note": "float64 flooding = the reference's algorithm and arithmetic, bit-exact "
-                    "(what nr_decode_ldpc / DLSCHDecode / ULSCH_decoding run)",
-            "roofline": {"bound": "valu",
-                         "achieved": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12, 3),
-                         "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
-                         "frac": round(B * EDGES * 8 * ALG_OPS_PER_EDGE / f64_launch / 1e12
-                                       / VALU_PEAK_TLANE, 4),
-                         "kernel": DEC64_KERNEL,
-                         "traffic": pmc_traffic(DEC64_KERNEL) if B == 4096 else None,
-                         "hbm_achieved_GBps": round(B * DEC64_BYTES_PER_CB / f64_launch / 1e9, 2),
-                         "algorithmic_bytes_per_cb": DEC64_BYTES_PER_CB,
-                         "note": "same 13 lane-ops per edge-update in float64 against the "
-                                 "full-rate lane peak (wall time incl. launch)"}}
-        del llr64
         # BASELINE config 2: encode-only
         dnb = torch.empty((B, N_TX), dtype=torch.int8, device=dev)
 

@@ -132,9 +132,11 @@ typedef struct {
 /* Decode a batch of codeblocks with heterogeneous (bgn, Zc) in at most two launches (one per
  * base graph).  `desc` is a HOST array of B descriptors; status[b] / iters[b] follow desc order.
  * The work list is built on the host and copied into a stream-ordered allocation
- * (hipMallocAsync / hipFreeAsync on `stream`) from a per-thread ring of 4 pinned staging buffers:
- * the call returns once the copy is queued; it blocks only if the copy issued from the same slot
- * 4 calls earlier has not completed yet.  Repeated decodes of one batch shape should build the
+ * (hipMallocAsync / hipFreeAsync on `stream`) from a per-thread pool of pinned staging buffers:
+ * the call returns once the copy is queued.  The pool grows with the plans in flight (a slot is
+ * reused once its copy has completed) up to 64 slots per thread, and only past 64 plans in flight
+ * does a call wait for the oldest copy.  The pool's pinned memory is held by each calling thread
+ * for the life of the process (about the size of its largest plans).  Repeated decodes of one batch shape should build the
  * plan once instead (ldpc5g_mixed_plan + ldpc5g_decode_ms_mixed_plan). */
 int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* llr_base,
                            int32_t llr_dtype, int8_t* ck_base, uint8_t* status, int32_t* iters,
@@ -250,7 +252,7 @@ int ldpc5g_sch_decode(const void* llr, int32_t llr_dtype, int64_t ldg, const ldp
  * bits used), g / llr [T][ldg] (E_total_t used), tbblk [T][ldb] (B_t used).
  * sizes[7] = {ck elements, dn elements, decoder-ck elements, codeblocks, max A, max B, max E}.
  * The per-TB geometry goes to the device like the mixed-Zc work list (stream-ordered allocation,
- * pinned staging ring: see ldpc5g_decode_ms_mixed). */
+ * pinned staging pool: see ldpc5g_decode_ms_mixed). */
 int ldpc5g_sch_multi_sizes(const ldpc5g_sch_cfg_t* cfgs, int32_t T, int64_t* sizes);
 int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
                             const ldpc5g_sch_cfg_t* cfgs, int32_t T, int8_t* ck, int8_t* dn,

@@ -3,6 +3,7 @@
 PyTorch-ROCm is used only for device memory and the current HIP stream; no torch ops run on
 the hot path.  There is no CPU fallback: if the library or a GPU is missing, calls raise.
 """
+import collections
 import ctypes
 import os
 import threading
@@ -193,19 +194,32 @@ def ptr(tensor):
 
 
 _tls = threading.local()
+STAGING_MAX = int(os.environ.get("LDPC5G_STAGING_MAX", "32"))
 
 
 def staging(key, make):
     """Per-thread cache of pinned-host / device buffers for the per-codeblock drop-ins (the
     reference's callers decode one codeblock per call, sim_ldpc_internal.py:51-58): a call then
-    costs one pinned H2D copy, the launch and one D2H copy, with no allocation."""
+    costs one pinned H2D copy, the launch and one D2H copy, with no allocation.  Bounded: at most
+    STAGING_MAX entries per thread, least recently used evicted (a sweep over MCS / TBS / PRB
+    configurations keeps only the recent ones; an evicted buffer is freed when its last user drops
+    it — torch's allocators order the reuse after the stream work that used it)."""
     d = getattr(_tls, "bufs", None)
     if d is None:
-        d = _tls.bufs = {}
+        d = _tls.bufs = collections.OrderedDict()
     b = d.get(key)
     if b is None:
         b = d[key] = make()
+        while len(d) > STAGING_MAX:
+            d.popitem(last=False)
+    else:
+        d.move_to_end(key)
     return b
+
+
+def staging_entries():
+    """Number of cached staging entries of this thread."""
+    return len(getattr(_tls, "bufs", ()))
 
 
 def to_device(a, key):

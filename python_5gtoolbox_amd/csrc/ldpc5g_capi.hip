@@ -41,10 +41,13 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 namespace {
-// Pinned staging ring for small host-built plans (stage_h2d).  A hipMemcpyAsync from pageable
+// Pinned staging pool for small host-built plans (stage_h2d).  A hipMemcpyAsync from pageable
 // memory may return before the runtime has read the source, so plans are first copied into a
-// pinned slot; the slot is reused only after the event recorded behind its copy has completed.
-// The slots are never freed (a thread-exit destructor could run after the HIP runtime is gone).
+// pinned slot; a slot is reused only after the event recorded behind its copy has completed.
+// The pool grows (up to kMaxSlots per thread) instead of waiting: a caller that queues many
+// decodes ahead of the GPU is throttled only past kMaxSlots plans in flight.  The slots are held
+// per thread for the life of the process, never freed (a thread-exit destructor could run after
+// the HIP runtime is gone); include/ldpc5g.h states it.
 struct PinnedSlot {
     void* buf = nullptr;
     size_t cap = 0;
@@ -52,21 +55,45 @@ struct PinnedSlot {
     int dev = -1;
     bool pending = false;
 };
-constexpr int kRing = 4;
-thread_local PinnedSlot t_ring[kRing];
-thread_local int t_next = 0;
+constexpr size_t kMaxSlots = 64;
+thread_local std::vector<PinnedSlot>* t_pool = nullptr;   // leaked on purpose (see above)
+thread_local size_t t_next = 0;
+
+// a free slot: one whose copy has completed (non-blocking query), else a new one, else wait for
+// the oldest-issued (round-robin) slot
+int take_slot(PinnedSlot** out) {
+    if (!t_pool) t_pool = new std::vector<PinnedSlot>();
+    std::vector<PinnedSlot>& pool = *t_pool;
+    for (size_t k = 0; k < pool.size(); ++k) {
+        PinnedSlot& s = pool[(t_next + k) % pool.size()];
+        if (s.pending && hipEventQuery(s.ev) == hipSuccess) s.pending = false;
+        if (!s.pending) {
+            t_next = (t_next + k + 1) % pool.size();
+            *out = &s;
+            return LDPC5G_OK;
+        }
+    }
+    if (pool.size() < kMaxSlots) {
+        pool.emplace_back();
+        *out = &pool.back();
+        return LDPC5G_OK;
+    }
+    PinnedSlot& s = pool[t_next];
+    t_next = (t_next + 1) % pool.size();
+    if (int rc = check_hip(hipEventSynchronize(s.ev), "hipEventSynchronize(staging)")) return rc;
+    s.pending = false;
+    *out = &s;
+    return LDPC5G_OK;
+}
 }  // namespace
 
 int stage_h2d(void* dst, const void* src, size_t n, hipStream_t st) {
     if (n == 0) return LDPC5G_OK;
     int dev = 0;
     if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
-    PinnedSlot& s = t_ring[t_next];
-    t_next = (t_next + 1) % kRing;
-    if (s.pending) {   // the copy queued from this slot kRing calls ago must have read it
-        if (int rc = check_hip(hipEventSynchronize(s.ev), "hipEventSynchronize(staging)")) return rc;
-        s.pending = false;
-    }
+    PinnedSlot* sp = nullptr;
+    if (int rc = take_slot(&sp)) return rc;
+    PinnedSlot& s = *sp;
     if (s.dev != dev && s.ev) {
         (void)hipEventDestroy(s.ev);
         s.ev = nullptr;

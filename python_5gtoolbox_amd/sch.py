@@ -192,7 +192,19 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
     T = llr.shape[0]
     ws = ws or SchWorkspace(cfg, T, llr.device)
     dn_dtype = dn_dtype or (t.float32 if schedule == "layered" else llr.dtype)
-    if algo == "min-sum":
+    if algo == "min-sum" and not beta >= 0:
+        # the reference decodes each codeblock with nr_decode_ldpc (nr_dlsch_decode.py:91,
+        # nr_ulsch_decode.py:92), which keeps min-sum's literal zero branches for beta < 0
+        # (nr_ldpc_decode.py:186-225): the sparse kernel on the base graph, as nr_decode_ldpc here
+        from .nr_ldpc_decode import SparseGraph, _sparse_graph, decode_ldpc_batch
+        llr_dn = sch_raterecover_batch(llr, cfg, harq_in, dn_dtype, ws)
+        x = t.zeros((T * cfg.C, cfg.N + 2 * cfg.Zc), dtype=t.float64, device=llr.device)
+        x[:, 2 * cfg.Zc:] = llr_dn   # punctured systematic columns: LLR 0 (nr_ldpc_decode.py:43)
+        g = _sparse_graph(("bg", cfg.bgn, cfg.Zc),
+                          lambda: SparseGraph.from_base_graph(cfg.bgn, cfg.Zc, llr.device), llr.device)
+        decode_ldpc_batch(x, g, L, algo, alpha, beta, out=(ws.dec_ck, ws.status, ws.iters))
+        sch_tb_check_batch(ws.dec_ck, cfg, T, ws)
+    elif algo == "min-sum":
         out = ws.dn_buf(dn_dtype, cfg)
         if harq_in is not None:
             assert harq_in.dtype == dn_dtype and harq_in.shape == out.shape and harq_in.is_contiguous()

@@ -10,11 +10,16 @@ ldpc5g_crc, encoder, torch's RNG for bits and noise) and decoded in one batched 
 stopping rule is evaluated at exactly the reference's counts, so each BLER point rests on the
 same number of trials as the reference's.
 
-Results are returned (and optionally written as JSON, not pickle) in the reference's shape:
-(sim_config, test_config_list, test_results_list).  run_ldpc_simulation_fixed is the fixed-count
-variant of scripts/sim_ldpc_decoder_bf.py (200 codeblocks per SNR below 4 dB, 2000 from 4 dB).
+run_ldpc_simulation writes the reference's result file — pickle.dump([sim_config,
+test_config_list, test_results_list]) — and returns None, so the reference's scripts
+(scripts/sim_ldpc_decoder.py:45-51 and the three alpha/beta searches) run unchanged once
+scripts.internal.sim_ldpc_internal points here (module sim_ldpc_internal); draw_ldpc_decoder_result
+plots it like :93-117.  run_ldpc_simulation_fixed is the fixed-count sweep of
+scripts/sim_ldpc_decoder_bf.py (200 codeblocks per SNR below 4 dB, 2000 from 4 dB).  simulate()
+returns the results together with the trial counts behind every value.
 """
 import json
+import pickle
 
 from . import _lib
 from .ldpc_info import code_dims
@@ -110,12 +115,13 @@ def bler_fixed(Zc, bgn, snr_db, crcpoly, algo, alpha, beta, L, n, gen, device, s
     return count, failed
 
 
-def run_ldpc_simulation_fixed(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list,
-                              L_list, snr_db_list, test_count_seed=200, filename=None, seed=0,
-                              schedule="flooding", verbose=False):
-    """The fixed-count BLER script scripts/sim_ldpc_decoder_bf.py:43-107 on the GPU: per SNR
-    total_count = test_count_seed if snr_db < 4 else 10 * test_count_seed (:77-80), same test
-    naming and result shape as run_ldpc_simulation."""
+def simulate(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list, L_list,
+             snr_db_list, seed=0, schedule="flooding", verbose=False, fixed_count=None):
+    """Run every test of the sweep; returns (sim_config, test_config_list, test_results_list,
+    trials) with trials[i][j] = [test_count, failed_count] behind test_results_list[i][j].
+    fixed_count=None: the reference's stopping rule (sim_ldpc_internal.py:44-83); else the
+    fixed-count loop of scripts/sim_ldpc_decoder_bf.py:74-98 (fixed_count codeblocks below 4 dB,
+    10x from 4 dB)."""
     t = _lib.require_gpu()
     dev = t.device("cuda", t.cuda.current_device())
     gen = t.Generator(device=dev)
@@ -126,39 +132,12 @@ def run_ldpc_simulation_fixed(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list
         flags.append(flag)
         bler, cnt = [], []
         for snr in snr_db_list:
-            total = test_count_seed if snr < 4 else test_count_seed * 10
-            n, f = bler_fixed(Zc, bgn, snr, crcpoly, algo, alpha, beta, L, total, gen, dev, schedule)
-            bler.append(f / n)
-            cnt.append([n, f])
-            if verbose:
-                print(f"finish test {flag}, snr_db={snr}, bler={f / n:2.5f}")
-        results.append(bler)
-        counts.append(cnt)
-    sim_config = {"Zc": Zc, "bgn": bgn}
-    if filename:
-        with open(filename, "w") as fh:
-            json.dump({"sim_config": sim_config, "test_config_list": flags,
-                       "test_results_list": results, "trials": counts,
-                       "snr_db_list": list(snr_db_list), "schedule": schedule}, fh, indent=1)
-    return sim_config, flags, results
-
-
-def run_ldpc_simulation(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list, L_list,
-                        snr_db_list, filename=None, seed=0, schedule="flooding", verbose=False):
-    """sim_ldpc_internal.run_ldpc_simulation on the GPU.  Returns (sim_config,
-    test_config_list, test_results_list); with `filename`, also writes them as JSON together with
-    the trial counts behind every BLER value."""
-    t = _lib.require_gpu()
-    dev = t.device("cuda", t.cuda.current_device())
-    gen = t.Generator(device=dev)
-    gen.manual_seed(seed)
-    flags, results, counts = [], [], []
-    for flag, algo, alpha, beta, L in test_configs(algo_list, alpha_list, beta_list, mixed_list,
-                                                   L_list):
-        flags.append(flag)
-        bler, cnt = [], []
-        for snr in snr_db_list:
-            n, f = bler_point(Zc, bgn, snr, crcpoly, algo, alpha, beta, L, gen, dev, schedule)
+            if fixed_count is None:
+                n, f = bler_point(Zc, bgn, snr, crcpoly, algo, alpha, beta, L, gen, dev, schedule)
+            else:
+                total = fixed_count if snr < 4 else fixed_count * 10
+                n, f = bler_fixed(Zc, bgn, snr, crcpoly, algo, alpha, beta, L, total, gen, dev,
+                                  schedule)
             bler.append(f / n)
             cnt.append([n, f])
             if verbose:
@@ -166,10 +145,69 @@ def run_ldpc_simulation(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixe
                       f"failed_count={f},bler={f / n:2.5f}")
         results.append(bler)
         counts.append(cnt)
-    sim_config = {"Zc": Zc, "bgn": bgn}
-    if filename:
-        with open(filename, "w") as fh:
+    return {"Zc": Zc, "bgn": bgn}, flags, results, counts
+
+
+def _dump(filename, json_filename, sim_config, flags, results, counts, snr_db_list, schedule):
+    # the reference's result file (sim_ldpc_internal.py:89-91): [sim_config, labels, bler lists],
+    # plain containers only, read back by the scripts with pickle.load (sim_ldpc_decoder.py:49-50)
+    with open(filename, "wb") as handle:
+        pickle.dump([sim_config, flags, results], handle, protocol=pickle.HIGHEST_PROTOCOL)
+    if json_filename:   # extra: the trial counts behind every BLER value
+        with open(json_filename, "w") as fh:
             json.dump({"sim_config": sim_config, "test_config_list": flags,
                        "test_results_list": results, "trials": counts,
                        "snr_db_list": list(snr_db_list), "schedule": schedule}, fh, indent=1)
-    return sim_config, flags, results
+
+
+def run_ldpc_simulation(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list, L_list,
+                        snr_db_list, filename, *, seed=0, schedule="flooding", verbose=True,
+                        json_filename=None):
+    """Drop-in for scripts/internal/sim_ldpc_internal.py:9-91 run_ldpc_simulation: the same
+    sweep (labels, order, stopping rule), batched on the GPU; writes
+    pickle.dump([sim_config, test_config_list, test_results_list]) to `filename` exactly as the
+    reference does and returns None.  The keyword-only extras: the RNG seed, the decoder
+    schedule ("flooding" = the reference's float64 arithmetic), per-point prints, and a JSON copy
+    with the trial counts."""
+    sim_config, flags, results, counts = simulate(Zc, bgn, crcpoly, algo_list, alpha_list,
+                                                  beta_list, mixed_list, L_list, snr_db_list,
+                                                  seed, schedule, verbose)
+    _dump(filename, json_filename, sim_config, flags, results, counts, snr_db_list, schedule)
+
+
+def run_ldpc_simulation_fixed(Zc, bgn, crcpoly, algo_list, alpha_list, beta_list, mixed_list,
+                              L_list, snr_db_list, filename, test_count_seed=200, *, seed=0,
+                              schedule="flooding", verbose=True, json_filename=None):
+    """The fixed-count sweep of scripts/sim_ldpc_decoder_bf.py:43-107 (its main body, which has no
+    function of its own in the reference): total_count = test_count_seed below 4 dB, 10x from
+    4 dB (:77-80); writes the same pickle to `filename` (:104-107) and returns None."""
+    sim_config, flags, results, counts = simulate(Zc, bgn, crcpoly, algo_list, alpha_list,
+                                                  beta_list, mixed_list, L_list, snr_db_list,
+                                                  seed, schedule, verbose,
+                                                  fixed_count=test_count_seed)
+    _dump(filename, json_filename, sim_config, flags, results, counts, snr_db_list, schedule)
+
+
+def draw_ldpc_decoder_result(snr_db_list, sim_config, test_config_list, test_results_list,
+                             figfile):
+    """scripts/internal/sim_ldpc_internal.py:93-117: BLER vs Eb/N0, one curve per test, log
+    scale, saved to `figfile` (host-only plotting, no GPU)."""
+    import matplotlib
+    if matplotlib.get_backend().lower() not in ("agg", "pdf", "svg", "ps", "cairo"):
+        matplotlib.use("Agg")   # headless: the reference saves to a file too (:115)
+    import matplotlib.pyplot as plt
+    fig = plt.figure()
+    markers = [".", "o", "v", "<", ">", "P", "*", "+", "x", "D", "d"]
+    plt.xlabel("Eb/N0")
+    plt.ylabel("BLER")
+    plt.title("ldpc decoder, Zc={}, bgn={}".format(sim_config["Zc"], sim_config["bgn"]))
+    plt.yscale("log")
+    plt.xlim(snr_db_list[0], snr_db_list[-1])
+    plt.ylim(10 ** (-4), 1)
+    plt.grid(True)
+    for i, label in enumerate(test_config_list):
+        plt.plot(snr_db_list, test_results_list[i], marker=markers[i % len(markers)],
+                 label="{}".format(label))
+    plt.legend(loc="upper right", fontsize=5)
+    plt.savefig(figfile)
+    plt.close(fig)

@@ -16,6 +16,7 @@ the float64 widening of those float32 values so the fixtures are exact for both 
   crc_golden.json      CRC KATs (the inline vectors of py5gphy/crc/crc.py:167-210) + generated
   dlsch_golden.npz     DLSCHEncode (nr_dlsch.py:12) transport blocks -> g_seq
   sch_golden.npz/.json DLSCHDecode (+HARQ), ULSCH encode/decode, a config-5 DLSCHEncode TB
+  sch_negbeta_golden.* DLSCHDecode / ULSCH_decoding with beta < 0 (per-codeblock nr_decode_ldpc)
   demod_golden.npz     nrModulate / nrDemodulate (QPSK..256QAM) / gen_nrPRBS vectors
   decode_bf_golden.npz / decode_bp_golden.npz   nr_decode_ldpc with algo='BF' / 'BP'
   sparse_golden.npz    decode_ldpc (nr_ldpc_decode.py:51) on random binary H (all algorithms), the
@@ -524,6 +525,41 @@ def gen_sch():
     print("sch cases", len(cases))
 
 
+def gen_sch_negbeta():
+    """DLSCHDecode / ULSCH_decoding with a negative offset beta: the reference decodes every
+    codeblock through nr_decode_ldpc (nr_dlsch_decode.py:91, nr_ulsch_decode.py:92), whose
+    min-sum keeps its literal zero branches for beta < 0 (nr_ldpc_decode.py:186-225)."""
+    from py5gphy.nr_pdsch import nr_dlsch, nr_dlsch_decode
+    from py5gphy.nr_pusch import nr_ulsch, nr_ulsch_decode
+    rng = np.random.default_rng(31)
+    cases, blobs = [], {}
+    specs = [("dl", 12000, 4, 517, 1, 0, 30000, 25000, 1.0, -0.25),
+             ("ul", 2000, 4, 200, 1, 3, 0, 9000, 0.0, -0.5)]
+    for n, (kind, TBS, Qm, R, NL, rv, LBRM, G, snr, beta) in enumerate(specs):
+        dec_cfg = {"L": 5, "algo": "min-sum", "alpha": 0.8, "beta": beta}
+        trblk = rng.integers(0, 2, TBS)
+        if kind == "dl":
+            g = nr_dlsch.DLSCHEncode(trblk, TBS, Qm, R, NL, rv, LBRM, G)
+        else:
+            cbs, Zc, bgn = nr_ulsch.ULSCH_Crc_CodeBlockSegment(trblk, TBS, R)
+            g = nr_ulsch.ULSCH_encoding_ratematch(cbs, Zc, bgn, Qm, G, NL, rv)
+        llr = bpsk_llr(g, snr, rng).astype(np.float32)
+        x = llr.astype(np.float64)
+        if kind == "dl":
+            ok, tbblk, new = nr_dlsch_decode.DLSCHDecode(x, TBS, Qm, R, NL, rv, LBRM, dec_cfg)
+        else:
+            ok, tbblk, new = nr_ulsch_decode.ULSCH_decoding(x, TBS, R, Qm, G, NL, rv, dec_cfg)
+        cases.append({"kind": kind, "TBS": TBS, "Qm": Qm, "R": R, "NL": NL, "rv": rv,
+                      "LBRM": LBRM, "G": G, "snr": snr, "dec": dec_cfg, "ok": bool(ok),
+                      "new_sha": _sha(new), "new_shape": list(new.shape)})
+        blobs[f"llr{n}"] = llr
+        blobs[f"tbblk{n}"] = np.packbits(np.asarray(tbblk).astype(np.uint8))
+        print("sch beta<0 case", n, kind, "ok", ok, flush=True)
+    np.savez_compressed(os.path.join(OUT, "sch_negbeta_golden.npz"), **blobs)
+    with open(os.path.join(OUT, "sch_negbeta_golden.json"), "w") as f:
+        json.dump(cases, f, indent=0)
+
+
 # ------------------------------------------------------- modulation / demodulation / PRBS (f4)
 def gen_demod():
     """nrModulate (common/nrModulation.py:4-41), nrDemodulate (demodulation/nr_Demodulation.py:
@@ -757,6 +793,8 @@ if __name__ == "__main__":
         gen_dlsch()
     if "sch" in which:
         gen_sch()
+    if "sch_negbeta" in which:
+        gen_sch_negbeta()
     if "demod" in which:
         gen_demod()
     if "decode" in which:

@@ -130,12 +130,45 @@ def test_layered_underattenuated_characterised():
     assert err[0.75, "layered"] <= err[0.75, "flooding"], err
 
 
+class _NoGlobals(__import__("pickle").Unpickler):
+    """Reads plain containers only: any class reference in the file raises."""
+    def find_class(self, module, name):
+        raise AssertionError(f"unexpected global {module}.{name}")
+
+
 def test_run_ldpc_simulation_shape(tmp_path):
-    from python_5gtoolbox_amd.sim_ldpc import run_ldpc_simulation
-    out = tmp_path / "sim.json"
-    cfg, flags, res = run_ldpc_simulation(12, 1, "24A", ["NMS", "OMS", "mixed-MS"], [0.7], [0.5],
-                                          [[0.8, 0.3]], [8], [3.0], str(out))
+    """The drop-in for scripts.internal.sim_ldpc_internal: run_ldpc_simulation(..., filename)
+    returns None and writes [sim_config, test_config_list, test_results_list] with pickle, which
+    the reference's scripts then pickle.load (scripts/sim_ldpc_decoder.py:45-51) and plot."""
+    import json
+    from python_5gtoolbox_amd import sim_ldpc_internal
+    out, js = tmp_path / "sim.pickle", tmp_path / "sim.json"
+    rv = sim_ldpc_internal.run_ldpc_simulation(12, 1, "24A", ["NMS", "OMS", "mixed-MS"], [0.7],
+                                               [0.5], [[0.8, 0.3]], [8], [3.0], str(out),
+                                               json_filename=str(js))
+    assert rv is None
+    with open(out, "rb") as fh:
+        cfg, flags, res = _NoGlobals(fh).load()
     assert cfg == {"Zc": 12, "bgn": 1}
     assert flags == ["NMS-alpha=0.7-L=8", "OMS-beta=0.5-L=8", "mixed-MS-[alpha,beta]=[0.8,0.3]-L=8"]
     assert len(res) == 3 and all(len(r) == 1 and 0.0 <= r[0] <= 0.01 for r in res)
-    assert out.exists()
+    assert all(type(r[0]) is float for r in res)
+    trials = json.load(open(js))["trials"]
+    assert all(t[0][0] in (1000, 2000, 4000, 10000) for t in trials)
+    sim_ldpc_internal.draw_ldpc_decoder_result([3.0, 3.5], cfg, flags, [r * 2 for r in res],
+                                               str(tmp_path / "fig.png"))
+    assert (tmp_path / "fig.png").stat().st_size > 0
+
+
+def test_run_ldpc_simulation_fixed_shape(tmp_path):
+    """The fixed-count sweep of scripts/sim_ldpc_decoder_bf.py: 200 codeblocks per SNR below
+    4 dB, 2000 from 4 dB, same pickle."""
+    import json
+    from python_5gtoolbox_amd import sim_ldpc_internal
+    out, js = tmp_path / "bf.pickle", tmp_path / "bf.json"
+    assert sim_ldpc_internal.run_ldpc_simulation_fixed(
+        10, 1, "24A", ["BF"], [], [], [], [16], [3.5, 4.0], str(out), json_filename=str(js)) is None
+    with open(out, "rb") as fh:
+        cfg, flags, res = _NoGlobals(fh).load()
+    assert cfg == {"Zc": 10, "bgn": 1} and flags == ["BF L=16"] and len(res[0]) == 2
+    assert [t[0] for t in json.load(open(js))["trials"][0]] == [200, 2000]

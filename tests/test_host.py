@@ -232,3 +232,41 @@ def test_sparse_scratch_sizing():
     assert lib.ldpc5g_sparse_scratch_bytes(2, 40000, 80000, 9, _lib.ALGO_BF) == 2 * 440000
     assert lib.ldpc5g_sparse_scratch_bytes(1, 4, 0, 12, _lib.ALGO_MS) == -1
     assert lib.ldpc5g_sparse_scratch_bytes(1, 4, 6, 12, 7) == -1
+
+
+def test_sim_harness_result_file_and_plot(tmp_path):
+    """Host side of the sim_ldpc_internal drop-in (no GPU): the result file is the reference's
+    pickle [sim_config, labels, bler lists] (scripts/internal/sim_ldpc_internal.py:89-91, plain
+    containers), and draw_ldpc_decoder_result (:93-117) plots a synthetic sweep to a file."""
+    import pickle
+    from python_5gtoolbox_amd import sim_ldpc, sim_ldpc_internal
+    cfg, flags = {"Zc": 12, "bgn": 1}, ["NMS-alpha=0.7-L=32", "mixed-MS-[alpha,beta]=[0.8,0.3]-L=32"]
+    res = [[0.395, 0.135, 0.015, 0.0005, 0.0], [0.275, 0.065, 0.00375, 0.0015, 0.0]]
+    snrs = [-1.0, -0.5, 0.0, 0.5, 1.0]
+    f = tmp_path / "r.pickle"
+    sim_ldpc._dump(str(f), None, cfg, flags, res, [[[1000, 1]] * 5] * 2, snrs, "flooding")
+
+    class NoGlobals(pickle.Unpickler):
+        def find_class(self, module, name):
+            raise AssertionError((module, name))
+    with open(f, "rb") as fh:
+        assert NoGlobals(fh).load() == [cfg, flags, res]
+    png = tmp_path / "r.png"
+    sim_ldpc_internal.draw_ldpc_decoder_result(snrs, cfg, flags, res, str(png))
+    assert png.read_bytes()[:4] == b"\x89PNG"
+
+
+def test_staging_cache_bounded():
+    """The drop-ins' per-thread staging cache (_lib.staging) keeps at most STAGING_MAX entries,
+    least recently used evicted: a sweep over many TB configurations cannot grow it without
+    bound."""
+    from python_5gtoolbox_amd import _lib
+    made = []
+    for i in range(3 * _lib.STAGING_MAX):
+        _lib.staging(("sweep", i), lambda: made.append(1) or object())
+        assert _lib.staging_entries() <= _lib.STAGING_MAX
+    assert len(made) == 3 * _lib.STAGING_MAX
+    last = ("sweep", 3 * _lib.STAGING_MAX - 1)
+    n = len(made)
+    _lib.staging(last, lambda: made.append(1) or object())   # cached: not rebuilt
+    assert len(made) == n

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, smoke, bench, rocprof kernel trace, encoder A/B probes and
 # PMC counter passes.  Usage (from the repo root, via gpurun):  bash tools/gpu_round.sh TAG [steps]
-#   steps: comma list of {tests,smoke,bench,trace,probe,pmc}; default all.
+#   steps: comma list of {tests,smoke,bench,trace,rehearse,probe,ab,pmc}; default tests,smoke,bench,trace,probe,pmc.
 # Every GPU step has its own time limit.  A test FAILURE (pytest rc 1) does not stop the script;
 # a crash, abort or time limit (any other non-zero rc) ends it at once.
 set -uo pipefail
@@ -36,19 +36,35 @@ fi
 if has trace; then
   echo "[gpu_round] rocprof kernel trace"
   cd /tmp
-  # headline only (--no-extras): the decoder's average in this summary is the bench's launch time
-  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_headline" -o run -- \
-      python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 --no-extras > "$OUT/bench_headline_under_rocprof.json" \
-      2> "$OUT/rocprof_headline.err" || { tail -20 "$OUT/rocprof_headline.err"; die trace $?; }
+  # headline only: the profiler records exactly the 20 timed launches (bench.py brackets them with
+  # roctxProfilerResume/Pause under LDPC5G_ROCTX=1 + --selected-regions), so the decoder's average
+  # in this summary is the launch time behind the bench's ms_per_step
+  LDPC5G_ROCTX=1 timeout -k 10 420 rocprofv3 --kernel-trace --stats --selected-regions --output-format csv \
+      -d "$OUT/prof_headline" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --no-reference \
+      > "$OUT/bench_headline_under_rocprof.json" 2> "$OUT/rocprof_headline.err" || { tail -20 "$OUT/rocprof_headline.err"; die trace $?; }
+  # the reference-precision line (float64 flooding), its timed launches only
+  LDPC5G_ROCTX=1 timeout -k 10 420 rocprofv3 --kernel-trace --stats --selected-regions --output-format csv \
+      -d "$OUT/prof_reference" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --roctx-region reference \
+      > "$OUT/bench_reference_under_rocprof.json" 2> "$OUT/rocprof_reference.err" || { tail -20 "$OUT/rocprof_reference.err"; die trace $?; }
   # everything (extras: encoder, flooding, config 4 / 5 chains): per-kernel table
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
       || { tail -20 "$OUT/rocprof.err"; die trace $?; }
   cd "$ROOT"
-  python tools/rocpd_summary.py "$OUT/prof_headline" --skip 3 > "$OUT/kernel_stats_headline.csv"
+  python tools/rocpd_summary.py "$OUT/prof_headline" > "$OUT/kernel_stats_headline.csv"
+  python tools/rocpd_summary.py "$OUT/prof_reference" > "$OUT/kernel_stats_reference.csv"
   python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
   cut -c1-150 "$OUT/kernel_stats_headline.csv" | head -6
+  cut -c1-150 "$OUT/kernel_stats_reference.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
+fi
+if has rehearse; then
+  echo "[gpu_round] 2-rank rehearsal (bench.py --gpus 2 --backend gloo: two ranks on one GPU)"
+  timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --no-extras --steps 10 --cpu-seconds 3 \
+      > "$OUT/bench_w2_gloo.json" 2> "$OUT/bench_w2_gloo.err" || { tail -20 "$OUT/bench_w2_gloo.err"; die rehearse $?; }
+  cat "$OUT/bench_w2_gloo.json"
+  timeout -k 10 120 python -u bench.py --gpus 8 --no-extras --cpu-seconds 0 > "$OUT/bench_w8_refused.json" 2> "$OUT/bench_w8_refused.err"
+  echo "bare --gpus 8 on one GPU: rc=$? $(cat "$OUT/bench_w8_refused.err")"
 fi
 if has probe; then
   echo "[gpu_round] throughput probes"
