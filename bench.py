@@ -122,9 +122,6 @@ def parse():
                     help="skip the secondary measurements (early exit, flooding, encoder)")
     ap.add_argument("--no-reference", action="store_true",
                     help="skip the float64 flooding (reference-precision) config-3 line")
-    ap.add_argument("--roctx-region", default="headline", choices=["headline", "reference"],
-                    help="timed region bracketed by roctxProfilerResume/Pause when LDPC5G_ROCTX=1 "
-                         "(rocprofv3 --selected-regions)")
     return ap.parse_args()
 
 
@@ -140,25 +137,9 @@ def make_llr(torch, enc, B, snr_db, seed, dev):
     return ck, dn, llr
 
 
-_ROCTX = []
-
-
-def roctx_region(on):
-    """With LDPC5G_ROCTX=1 (set by tools/gpu_round.sh for `rocprofv3 --selected-regions`), resume /
-    pause the profiler around a timed region, so the committed kernel statistics hold exactly the
-    timed launches (no warmup launches in the average)."""
-    if os.environ.get("LDPC5G_ROCTX") != "1":
-        return
-    if not _ROCTX:
-        import ctypes
-        _ROCTX.append(ctypes.CDLL("librocprofiler-sdk-roctx.so"))
-    (_ROCTX[0].roctxProfilerResume if on else _ROCTX[0].roctxProfilerPause)(0)
-
-
-def timed(torch, dist, world, fn, steps, warmup, region=False):
+def timed(torch, dist, world, fn, steps, warmup):
     """warmup, then exactly `steps` calls bracketed by barrier + synchronize; returns
-    (max-over-ranks wall seconds, this rank's event-timed seconds).  region: the profiler's
-    selected region (roctx_region) is exactly these `steps` launches."""
+    (max-over-ranks wall seconds, this rank's event-timed seconds)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -167,16 +148,12 @@ def timed(torch, dist, world, fn, steps, warmup, region=False):
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
-    if region:
-        roctx_region(True)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(steps):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    if region:
-        roctx_region(False)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -469,8 +446,7 @@ def bench_reference_precision(torch, dist, world, llr, out, args, cpu64):
     def step():
         D = sys.modules["python_5gtoolbox_amd.nr_ldpc_decode"]
         D.nr_decode_ldpc_batch(llr64, ZC, BG, args.L, "min-sum", args.alpha, 0.0, "flooding", out=out)
-    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup,
-                     region=args.roctx_region == "reference")
+    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup)
     iters = out[2].float().mean().item()
     launch_s = ev / args.steps
     edge_rate = B * EDGES * iters / launch_s
@@ -596,8 +572,7 @@ def main():
         D.nr_decode_ldpc_batch(llr, ZC, BG, args.L, "min-sum", args.alpha, 0.0, args.schedule,
                                out=out)
 
-    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup,
-                     region=args.roctx_region == "headline")
+    wall, ev = timed(torch, dist, world, step, args.steps, args.warmup)
     iters = out[2].float().mean().item()
     conv = int(out[1].sum().item())
     total_cb = B * world * args.steps

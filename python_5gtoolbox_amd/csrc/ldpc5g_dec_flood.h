@@ -30,6 +30,16 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 #endif
 // extension-column LLRs are loaded this many ext rows ahead of their use in phase A
 constexpr int kXPre = LDPC5G_FLOOD_XPRE;
+// phase A: core-edge LQ reads issued this many edges ahead (0: at their use), and whether a
+// scheduling barrier pins each read before the arithmetic of the edge it overlaps
+#ifndef LDPC5G_FLOOD_APRE
+#define LDPC5G_FLOOD_APRE 0
+#endif
+#ifndef LDPC5G_FLOOD_ASB
+#define LDPC5G_FLOOD_ASB 0
+#endif
+constexpr int kAPre = LDPC5G_FLOOD_APRE;
+constexpr bool kASb = LDPC5G_FLOOD_ASB != 0;
 
 // Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
 // state lives, and the packing of its sign word.  NP = 2, CS = 384 for batches; NP = 16, CS = 64 for
@@ -416,6 +426,16 @@ __device__ __forceinline__ void flood_body(
             T min1 = FT<T>::inf(), min2 = FT<T>::inf();
             uint32_t sx = 0, idx = 0, negs = 0;
             bool par = false;
+            // core-edge LQ reads issued kAPre edges ahead of their use (ring ab)
+            constexpr int AP = kAPre > 0 ? kAPre : 1;
+            T ab[AP];
+            auto aload = [&](auto kc2) {
+                constexpr int k2 = decltype(kc2)::value;
+                if constexpr (kAPre > 0 && k2 < d) {
+                    if constexpr (P::COL[e0 + k2] < KC) ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + rot(sh(e0 + k2)));
+                }
+            };
+            sfor<0, AP>([&](auto kc2) { aload(kc2); });
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int j = P::COL[e0 + k];
@@ -423,7 +443,13 @@ __device__ __forceinline__ void flood_body(
                 asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
                 T a;
                 if constexpr (j < KC) {
-                    a = at(j * CS * TS + rot(sh(e0 + k)));
+                    if constexpr (kAPre > 0) {
+                        a = ab[k % AP];
+                        aload(std::integral_constant<int, k + AP>{});
+                        if constexpr (kASb) __builtin_amdgcn_sched_barrier(0);
+                    } else {
+                        a = at(j * CS * TS + rot(sh(e0 + k)));
+                    }
                 } else {
                     constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
                     if constexpr (kXPre > 0) {

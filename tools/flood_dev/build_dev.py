@@ -39,6 +39,19 @@ VARIANTS = {
 }
 
 
+# compile-time flags per variant (the product header's LDPC5G_FLOOD_* knobs)
+FLAGS = {
+    "pre1": ["-DLDPC5G_FLOOD_APRE=1"],
+    "pre2": ["-DLDPC5G_FLOOD_APRE=2"],
+    "pre3": ["-DLDPC5G_FLOOD_APRE=3"],
+    "pre1sb": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=1"],
+    "pre2sb": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=1"],
+    "pre3sb": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=1"],
+}
+for _n in FLAGS:
+    VARIANTS.setdefault(_n, [])
+
+
 def make(name):
     d = os.path.join(ROOT, "build", "fdev", name)
     shutil.rmtree(d, ignore_errors=True)
@@ -55,7 +68,7 @@ def make(name):
         open(p, "w").write(s)
     out = os.path.join(ROOT, "build", "fdev", name + ".so")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-           "-shared", f"-I{ROOT}/include", f"-I{d}", *os.environ.get("FDEV_FLAGS", "").split(),
+           "-shared", f"-I{ROOT}/include", f"-I{d}", *os.environ.get("FDEV_FLAGS", "").split(), *FLAGS.get(name, []),
            os.path.join(HERE, "fdev.hip"), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     return name, r.returncode, r.stderr[-3000:]

@@ -36,27 +36,31 @@ fi
 if has trace; then
   echo "[gpu_round] rocprof kernel trace"
   cd /tmp
-  # headline only: the profiler records exactly the 20 timed launches (bench.py brackets them with
-  # roctxProfilerResume/Pause under LDPC5G_ROCTX=1 + --selected-regions), so the decoder's average
-  # in this summary is the launch time behind the bench's ms_per_step
-  LDPC5G_ROCTX=1 timeout -k 10 420 rocprofv3 --kernel-trace --stats --selected-regions --output-format csv \
+  # headline only (the bench's 3 warmup + 20 timed launches; the summary skips the warmups, so the
+  # decoder's average is over the launches behind the bench's ms_per_step)
+  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$OUT/prof_headline" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --no-reference \
       > "$OUT/bench_headline_under_rocprof.json" 2> "$OUT/rocprof_headline.err" || { tail -20 "$OUT/rocprof_headline.err"; die trace $?; }
-  # the reference-precision line (float64 flooding), its timed launches only
-  LDPC5G_ROCTX=1 timeout -k 10 420 rocprofv3 --kernel-trace --stats --selected-regions --output-format csv \
-      -d "$OUT/prof_reference" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --roctx-region reference \
+  # the reference-precision line (float64 flooding): its kernel runs only in that line
+  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d "$OUT/prof_reference" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras \
       > "$OUT/bench_reference_under_rocprof.json" 2> "$OUT/rocprof_reference.err" || { tail -20 "$OUT/rocprof_reference.err"; die trace $?; }
   # everything (extras: encoder, flooding, config 4 / 5 chains): per-kernel table
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
       || { tail -20 "$OUT/rocprof.err"; die trace $?; }
   cd "$ROOT"
-  python tools/rocpd_summary.py "$OUT/prof_headline" > "$OUT/kernel_stats_headline.csv"
-  python tools/rocpd_summary.py "$OUT/prof_reference" > "$OUT/kernel_stats_reference.csv"
+  python tools/rocpd_summary.py "$OUT/prof_headline" --skip 3 > "$OUT/kernel_stats_headline.csv"
+  python tools/rocpd_summary.py "$OUT/prof_reference" --skip 3 > "$OUT/kernel_stats_reference.csv"
   python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
   cut -c1-150 "$OUT/kernel_stats_headline.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats_reference.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
+fi
+if has fdev; then
+  echo "[gpu_round] float64 flooding variants (build/fdev/*.so)"
+  timeout -k 10 300 python -u tools/flood_dev/run_dev.py ${FDEV_LIBS:-build/fdev/*.so} > "$OUT/fdev.log" 2>&1 || { tail -20 "$OUT/fdev.log"; die fdev $?; }
+  grep -v amdgpu.ids "$OUT/fdev.log"
 fi
 if has rehearse; then
   echo "[gpu_round] 2-rank rehearsal (bench.py --gpus 2 --backend gloo: two ranks on one GPU)"
