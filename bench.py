@@ -313,11 +313,42 @@ def bench_dlsch_caller(rank, reps=5):
             "codec_only_ms_per_codeblock": round(res["codec_only_swap_ms_per_tb"] / 23, 3)}
 
 
+def ev_ms(torch, fn, reps=5):
+    """Event-timed milliseconds per call of fn (one untimed call first), on torch's current
+    stream — the stream the library launches on."""
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def hbm_line(alg_bytes, ms):
+    """Algorithmic-byte roofline of one kernel call: bytes it must move / its event time."""
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    return {"ms": round(ms, 4), "algorithmic_bytes": int(alg_bytes), "achieved_GBps": round(gbs, 1),
+            "peak_GBps": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4), "bound": "hbm"}
+
+
+def valu_line(edges, ms):
+    """Lane-op roofline of a decode call: 13 lane-ops per edge-update."""
+    t = edges * ALG_OPS_PER_EDGE / (ms * 1e-3) / 1e12
+    return {"ms": round(ms, 4), "edge_updates": int(edges), "achieved": round(t, 3),
+            "peak": round(VALU_PEAK_TLANE, 1), "unit": "T lane-op/s",
+            "frac": round(t / VALU_PEAK_TLANE, 4), "bound": "valu"}
+
+
 def bench_config4(torch, dist, world, dev, rank, steps):
     """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
     (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
     GPU chain (encode -> rate match -> BPSK+AWGN -> rate recover), OMS beta=0.5, L=8, decoded by
-    ldpc5g_decode_ms_mixed (one call, two launches: BG1 / BG2 work lists)."""
+    ldpc5g_decode_ms_mixed (one call, two launches: BG1 / BG2 work lists).  The timed step is the
+    decode; the rate recovery of the 12 groups is timed beside it (per-kernel split)."""
     import numpy as np
     from python_5gtoolbox_amd.ldpc_info import code_dims
     from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
@@ -327,7 +358,7 @@ def bench_config4(torch, dist, world, dev, rank, steps):
     g = torch.Generator(device=dev)
     g.manual_seed(404 + rank)
     n_per, snr = 341, 1.0
-    groups, info_bits = [], 0
+    groups, info_bits, rr, rr_bytes, edges = [], 0, [], 0, 0
     for Zc in (12, 40, 72, 176, 208, 384):
         for bg in (1, 2):
             K, N, _ = code_dims(bg, Zc)
@@ -341,21 +372,37 @@ def bench_config4(torch, dist, world, dev, rank, steps):
             y = (1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g)
             llr = (2 * y / sigma ** 2).contiguous()
             dn = sch_raterecover_batch(llr, cfg, dn_dtype=torch.float32).clone()
+            rr.append((llr, cfg))
+            rr_bytes += n_per * (4 * E + 4 * N)   # LLRs in, rate-recovered row out (float32)
+            edges += n_per * (316 if bg == 1 else 197) * Zc
             groups.append((bg, Zc, dn))
             info_bits += n_per * K
     mb = MixedBatch(groups)
     B = mb.B
     # rate-recovered rows: untransmitted parity columns are +0.0 (LDPC5G_RATE_MATCHED)
-    wall, _ = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered", True), steps, 2)
+    wall, ev = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered", True), steps, 2)
     _, st, it = mb.decode(8, 1.0, 0.5, "layered", True)
+    mean_it = it.float().mean().item()
+    rr_ms = ev_ms(torch, lambda: [sch_raterecover_batch(x, c, dn_dtype=torch.float32)
+                                  for x, c in rr])
     return {"workload": "BASELINE config 4: 12 (Zc, BG) groups x 341 CBs, random (Qm, rv, E), "
                         "GPU rate match/recover, snr 1 dB, layered OMS beta=0.5 L=8, "
                         "LDPC5G_RATE_MATCHED",
             "codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
             "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
             "ms_per_call": round(wall / steps * 1e3, 4),
-            "mean_iterations": round(it.float().mean().item(), 3),
-            "converged_frac": round(st.float().mean().item(), 4)}
+            "mean_iterations": round(mean_it, 3),
+            "converged_frac": round(st.float().mean().item(), 4),
+            "kernels": {
+                "decode": {**valu_line(edges * mean_it, ev / steps * 1e3),
+                           "note": "edge-updates of the full graphs x mean iterations; rows whose "
+                                   "extension column was never transmitted are skipped by the "
+                                   "kernel (LDPC5G_RATE_MATCHED), so this counts more work than "
+                                   "it does"},
+                "raterecover": {**hbm_line(rr_bytes, rr_ms),
+                                "note": "the 12 groups' sch_raterecover_batch calls (float32 in, "
+                                        "float32 rows out: 4E + 4N bytes per codeblock); not in "
+                                        "the timed step"}}}
 
 
 def bench_config5(torch, dist, world, dev, rank, steps, T=32):
@@ -363,10 +410,13 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     129 BG1 Zc=384 codeblocks per TB, G = 8*4*36036), T TBs per GPU, every step on the GPU:
     TX = ldpc5g_sch_encode + scrambling/256QAM mapping; RX = soft demodulation/descrambling +
     ldpc5g_sch_decode (rate recovery, layered NMS L=8, CB/TB CRCs).  Channel: complex AWGN on the
-    symbols at 30 dB (outside the timed regions)."""
+    symbols (outside the timed regions), at 30 dB (easy: ~3 iterations) and at the threshold point
+    (the highest SNR of a list at which the decoder needs >= 6 mean iterations, the same SNR on
+    every rank), each with its TB CRC pass rate; per-kernel split + rooflines at the threshold."""
     from python_5gtoolbox_amd import phy
+    from python_5gtoolbox_amd.nr_ldpc_decode import nr_decode_ldpc_batch
     from python_5gtoolbox_amd.sch import SchWorkspace, sch_config, sch_decode_batch, \
-        sch_encode_batch
+        sch_encode_batch, sch_raterecover_batch, sch_tb_check_batch
     from python_5gtoolbox_amd.shard import decode_tbs_sharded
     A, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
     cfg = sch_config(A, Qm, R, NL, rv, A, G)
@@ -382,19 +432,21 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
         phy.scramble_modulate(bits, Qm, cinit, out=sym)
     wt, _ = timed(torch, dist, world, tx, steps, 2)
     tx()
-    snr = 30.0
-    nvar = 10 ** (-snr / 10)
-    noise = torch.complex(torch.randn(sym.shape, device=dev, generator=g),
-                          torch.randn(sym.shape, device=dev, generator=g)) * (nvar / 2) ** 0.5
-    y = (sym + noise).contiguous()
-    del noise
-    nv = torch.full(sym.shape, nvar, dtype=torch.float32, device=dev)
     llr = torch.empty((T, G), dtype=torch.float32, device=dev)
+    cur = {}
+
+    def channel(snr):
+        nvar = 10 ** (-snr / 10)
+        noise = torch.complex(torch.randn(sym.shape, device=dev, generator=g),
+                              torch.randn(sym.shape, device=dev, generator=g)) * (nvar / 2) ** 0.5
+        cur["y"] = (sym + noise).contiguous()
+        del noise
+        cur["nv"] = torch.full(sym.shape, nvar, dtype=torch.float32, device=dev)
 
     last = {}
 
     def rx_local(y_local):
-        phy.demod_descramble(y_local, nv, Qm, cinit, out=llr)
+        phy.demod_descramble(y_local, cur["nv"], Qm, cinit, out=llr)
         r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
         last["r"] = r
         return r.tb_ok, r.tbblk
@@ -404,28 +456,81 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
     def rx():
         # this rank's TBs (round robin over T*world) -> records -> ONE RCCL gather to rank 0
         if gather:
-            return decode_tbs_sharded(y, cfg, 8, T_total=T * world, decode_fn=rx_local, timing=tm)
-        return rx_local(y)
-    wr, _ = timed(torch, dist, world, rx, steps, 2)
-    res = rx()
-    r = last["r"]
-    ok = bool(torch.equal(r.tbblk[:, :A], tb))
-    if gather and rank == 0:   # rank 0's own TBs, back through pack -> gather -> unpack
-        ok = ok and bool(torch.equal(res[1][0::world][:, :A], tb)) and \
-            bool(torch.equal(res[0][0::world], r.tb_ok.to(torch.uint8)))
+            return decode_tbs_sharded(cur["y"], cfg, 8, T_total=T * world, decode_fn=rx_local,
+                                      timing=tm)
+        return rx_local(cur["y"])
+
+    def rx_line(snr):
+        channel(snr)
+        wr, _ = timed(torch, dist, world, rx, steps, 2)
+        res = rx()
+        r = last["r"]
+        ok = r.tb_ok.bool()
+        # TBs that pass their CRC carry the transmitted bits
+        good = bool(torch.equal(r.tbblk[:, :A][ok], tb[ok]))
+        if gather and rank == 0:   # rank 0's own TBs, back through pack -> gather -> unpack
+            good = good and bool(torch.equal(res[1][0::world][:, :A][ok], tb[ok])) and \
+                bool(torch.equal(res[0][0::world], r.tb_ok.to(torch.uint8)))
+        return {"snr_db": snr, "rx_tb_per_s": round(T * world * steps / wr, 2),
+                "rx_codeblocks_per_s": round(T * cfg.C * world * steps / wr, 1),
+                "rx_info_gbit_s": round(T * A * world * steps / wr / 1e9, 3),
+                "rx_ms_per_batch": round(wr / steps * 1e3, 4),
+                "tb_crc_ok_frac": round(ok.float().mean().item(), 4),
+                "tb_bits_match_where_crc_ok": good,
+                "mean_iterations": round(r.iters.float().mean().item(), 3)}
+
+    easy = rx_line(30.0)
+    # threshold search (untimed): mean decoder iterations per candidate SNR, averaged over ranks
+    cands = [24.0, 23.5, 23.0, 22.5, 22.0, 21.5, 21.0, 20.5, 20.0, 19.0, 18.0]
+    its = []
+    for snr in cands:
+        channel(snr)
+        rx_local(cur["y"])
+        its.append(last["r"].iters.float().mean().item())
+    if world > 1:
+        v = torch.tensor(its, dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(v)
+        its = (v / world).tolist()
+    pick = next((c for c, m in zip(cands, its) if m >= 6.0), cands[-1])
+    thr = rx_line(pick)
+    # per-kernel split at the threshold point (event-timed, the same calls rx makes)
+    y = cur["y"]
+    t_demod = ev_ms(torch, lambda: phy.demod_descramble(y, cur["nv"], Qm, cinit, out=llr))
+    dn = sch_raterecover_batch(llr, cfg, None, torch.float32, ws)
+    t_rr = ev_ms(torch, lambda: sch_raterecover_batch(llr, cfg, None, torch.float32, ws))
+    dec_out = (ws.dec_ck, ws.status, ws.iters)
+    t_dec = ev_ms(torch, lambda: nr_decode_ldpc_batch(dn, cfg.Zc, cfg.bgn, 8, "min-sum", 0.75, 0.0,
+                                                      "layered", out=dec_out, rate_matched=True))
+    t_chk = ev_ms(torch, lambda: sch_tb_check_batch(ws.dec_ck, cfg, T, ws))
+    n_sym, ncb = T * (G // Qm), T * cfg.C
+    it_mean = ws.iters.float().mean().item()
+    split = {
+        "demod_descramble": {**hbm_line(n_sym * (8 + 4) + T * G * 4 + 2 * T * G // 8, t_demod),
+                             "note": "complex64 symbol + float32 noise variance in, Qm float32 "
+                                     "LLRs out, packed scrambling words written + read (PRBS "
+                                     "kernel included)"},
+        "raterecover": {**hbm_line(T * cfg.E_total * 4 + ncb * cfg.N * 4, t_rr),
+                        "note": "E float32 LLRs in, N float32 rate-recovered LLRs out per CB"},
+        "decode": {**valu_line(ncb * 316 * cfg.Zc * it_mean, t_dec),
+                   "mean_iterations": round(it_mean, 3),
+                   "note": "layered, LDPC5G_RATE_MATCHED (dead extension rows skipped: fewer "
+                           "edge-updates done than counted)"},
+        "tb_check": hbm_line(ncb * (cfg.K_apo + cfg.cbz), t_chk),
+    }
+    split["sum_ms"] = round(t_demod + t_rr + t_dec + t_chk, 4)
     return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, 256QAM, BG1 Zc=384, "
-                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN {snr} dB",
+                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN",
             "tb_per_gpu": T, "codeblocks_per_tb": cfg.C,
-            "rx_tb_per_s": round(T * world * steps / wr, 2),
-            "rx_codeblocks_per_s": round(T * cfg.C * world * steps / wr, 1),
-            "rx_info_gbit_s": round(T * A * world * steps / wr / 1e9, 3),
-            "rx_ms_per_batch": round(wr / steps * 1e3, 4),
+            **{k: easy[k] for k in ("rx_tb_per_s", "rx_codeblocks_per_s", "rx_info_gbit_s",
+                                    "rx_ms_per_batch", "tb_crc_ok_frac", "mean_iterations")},
+            "snr_db": easy["snr_db"], "tb_bits_match": easy["tb_bits_match_where_crc_ok"],
             "tx_tb_per_s": round(T * world * steps / wt, 2),
             "tx_info_gbit_s": round(T * A * world * steps / wt / 1e9, 3),
             "tx_ms_per_batch": round(wt / steps * 1e3, 4),
-            "tb_crc_ok_frac": round(r.tb_ok.float().mean().item(), 4),
-            "tb_bits_match": ok,
-            "mean_iterations": round(r.iters.float().mean().item(), 3),
+            "threshold": {**thr, "search": {"snr_db": cands,
+                                           "mean_iterations": [round(m, 3) for m in its]},
+                          "kernels": split},
             "gather": ({"what": "TB round robin over ranks; (tb_ok, tbblk) packed into "
                                 f"{tm.get('gather_bytes', 0) // max(world, 1) // max(T, 1)}-B records, "
                                 "ONE dist.gather (RCCL) to rank 0, unpacked there — inside rx",

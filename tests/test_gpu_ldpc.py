@@ -173,6 +173,28 @@ def test_decode_flooding_small_launch(torch, dec, bg, Zc, B, dtype):
         assert np.array_equal(g, r)
 
 
+@pytest.mark.parametrize("bg,Zc,B", [(1, 64, 1), (2, 64, 1), (2, 8, 8), (1, 2, 32), (1, 40, 1)])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_decode_small_kernel_edge_cases(torch, dec, bg, Zc, B, dtype):
+    """The small-codeblock kernel (ldpc5g_dec_small.h, B * Zc <= 64) on its edge cases, bit-exact
+    with the oracle: NMS (beta 0) and OMS, L = 0 / 1 / 8, integer LLRs (|q| ties, argmin order),
+    an all-zero codeblock and a noiseless one (exit at iteration 0)."""
+    rng = np.random.default_rng(Zc * 7 + B)
+    K = (22 if bg == 1 else 10) * Zc
+    ck = rng.integers(0, 2, (B, K)).astype(np.int8)
+    dn = O.encode(ck, bg)
+    llr = (1 - 2 * dn) * 2.0 + rng.integers(-3, 4, dn.shape)   # integer: ties everywhere
+    llr[0] = 0.0
+    if B > 1:
+        llr[1] = (1 - 2 * dn[1]) * 4.0
+    llr = llr.astype(dtype)
+    for L, alpha, beta in ((0, 0.75, 0.0), (1, 1.0, 0.5), (8, 0.8, 0.0), (8, 1.0, 0.25)):
+        got = dec.nr_decode_ldpc_batch(llr, Zc, bg, L, "min-sum", alpha, beta, "flooding")
+        ref = O.decode_flooding(llr, Zc, bg, L, alpha, beta, dtype)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r), (L, alpha, beta)
+
+
 @pytest.mark.parametrize("schedule,dtype", [("flooding", np.float32), ("layered", np.float32),
                                             ("flooding", np.float64)])
 def test_decode_z384_batch_vs_oracle(torch, dec, schedule, dtype):

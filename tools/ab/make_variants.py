@@ -228,6 +228,84 @@ def _ts(flood):
 
 
 VARIANTS.update({"lay_ts": (LAYERED, _ts(False)), "flood_ts": (FLOOD, _ts(True))})
+# the per-thread output / LLR row of the layered kernel re-derived after the iteration loop from an
+# opaque thread id, instead of keeping crow / out / lrow copies live across the loop (they were
+# the kernel's only scratch spills: 40 B/lane, 63 MB of WRITE per 4096-codeblock launch)
+_REDERIVE = [
+    ("""                if (cand && flagB[cl] == 0) {
+                    if (z == 0) status[out] = 1, iters[out] = it + 1;""",
+     """                if (cand && flagB[cl] == 0) {
+                    if (z == 0) {
+                        int tq = t;
+                        asm volatile("" : "+v"(tq));
+                        const int cq = tq - zv * G;
+                        const int oq = work ? cbs[work[blockIdx.x].first + cq].out : (int)blockIdx.x * G + cq;
+                        status[oq] = 1, iters[oq] = it + 1;
+                    }"""),
+    ("""    zv = z;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    if (active) {""",
+     """    zv = z;
+    asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    int t2 = t;
+    asm volatile("" : "+v"(t2));
+    const int cl2 = t2 - zv * G;   // zv = z here (no division)
+    int out2 = 0;
+    const T* lrow2 = llr;
+    if (valid) {
+        if (work) {
+            const CbRef r2 = cbs[work[blockIdx.x].first + cl2];
+            out2 = r2.out, lrow2 = llr + r2.llr_off;
+        } else {
+            out2 = (int)blockIdx.x * G + cl2, lrow2 = llr + (int64_t)out2 * ldl;
+        }
+    }
+    auto llrx2 = [&](int i4) -> T { return lrow2[(KB + 4 + i4 - pc) * Zc + zv]; };
+    if (active) {"""),
+    ("""            sfor<x0, x1>([&](auto xc) { vx[decltype(xc)::value - x0] = llrx(decltype(xc)::value); });""",
+     """            sfor<x0, x1>([&](auto xc) { vx[decltype(xc)::value - x0] = llrx2(decltype(xc)::value); });"""),
+    ("""        if (fail) flagA[cl] = 1;
+        uint32_t oc = 0;""", """        if (fail) flagA[cl2] = 1;
+        uint32_t oc = 0;"""),
+    ("""    if (active && z == 0) {
+        status[out] = flagA[cl] == 0;
+        iters[out] = L;
+    }""", """    if (active && z == 0) {
+        status[out2] = flagA[cl2] == 0;
+        iters[out2] = L;
+    }"""),
+    ("""            const uint32_t sb = (uint32_t)(cl * ck_stage_stride(NFZ) + zv);""",
+     """            const uint32_t sb = (uint32_t)(cl2 * ck_stage_stride(NFZ) + zv);"""),
+    ("""        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow));   // orders the staging too""",
+     """        int8_t* crow2 = ck;
+        if (valid) crow2 = work ? ck + cbs[work[blockIdx.x].first + cl2].ck_off : ck + (int64_t)out2 * ldc;
+        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow2));   // orders the staging too"""),
+]
+# ... and the stop rule's flag slot from the per-iteration opaque zv (its address was hoisted out of
+# the loop and spilled)
+_REDERIVE_FLAGS = [
+    ("""        {
+            // ---- layered stopping rule: no hard decision changed over the iteration, then an
+            //      exact syndrome check of those decisions (oracle.decode_layered)
+            uint32_t hdc = 0;""", """        const int clq = valid ? t - zv * G : 0;
+        {
+            // ---- layered stopping rule: no hard decision changed over the iteration, then an
+            //      exact syndrome check of those decisions (oracle.decode_layered)
+            uint32_t hdc = 0;"""),
+    ("""            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;""",
+     """            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[clq] = 1;"""),
+    ("""            const bool cand = active && flagA[cl] == 0;""", """            const bool cand = active && flagA[clq] == 0;"""),
+    ("""                    if (sf) flagB[cl] = 1;""", """                    if (sf) flagB[clq] = 1;"""),
+    ("""                if (cand && flagB[cl] == 0) {""", """                if (cand && flagB[clq] == 0) {"""),
+    ("""        lds_barrier();
+        if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+        if (!block_any(active)) break;""", """        lds_barrier();
+        if (z == 0 && valid) flagA[clq] = 0, flagB[clq] = 0;
+        if (!block_any(active)) break;"""),
+]
+VARIANTS.update({"lay_rederive": (LAYERED, _REDERIVE), "lay_rederive2": (LAYERED, _REDERIVE + _REDERIVE_FLAGS)})
+# unified diffs against python_5gtoolbox_amd/csrc (applied with patch -p3 in the copy)
+VARIANTS.update({"lay_bitsyn": (LAYERED, "tools/ab/bitsyn_final_syndrome.patch")})
 
 
 def make(name):
@@ -236,11 +314,16 @@ def make(name):
     shutil.rmtree(d, ignore_errors=True)
     shutil.copytree(CSRC, d)
     p = os.path.join(d, target)
-    s = open(p).read()
-    for old, new in patches:
-        assert old in s, (name, old[:60])
-        s = s.replace(old, new)
-    open(p, "w").write(s)
+    if isinstance(patches, str):
+        with open(os.path.join(ROOT, patches)) as f:
+            r = subprocess.run(["patch", "-p3", "-d", d], stdin=f, capture_output=True, text=True)
+        assert r.returncode == 0, (name, r.stdout, r.stderr)
+    else:
+        s = open(p).read()
+        for old, new in patches:
+            assert old in s, (name, old[:60])
+            s = s.replace(old, new)
+        open(p, "w").write(s)
     out = os.path.join(ROOT, "build", "alt", name + ".so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if target == LAYERED and name.startswith("lay"):

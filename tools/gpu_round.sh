@@ -62,6 +62,11 @@ if has fdev; then
   timeout -k 10 300 python -u tools/flood_dev/run_dev.py ${FDEV_LIBS:-build/fdev/*.so} > "$OUT/fdev.log" 2>&1 || { tail -20 "$OUT/fdev.log"; die fdev $?; }
   grep -v amdgpu.ids "$OUT/fdev.log"
 fi
+if has small; then
+  echo "[gpu_round] small-codeblock latency probe"
+  timeout -k 10 180 python -u tools/probe_small.py > "$OUT/probe_small.log" 2>&1 || { tail -20 "$OUT/probe_small.log"; die small $?; }
+  grep -v amdgpu.ids "$OUT/probe_small.log"
+fi
 if has rehearse; then
   echo "[gpu_round] 2-rank rehearsal (bench.py --gpus 2 --backend gloo: two ranks on one GPU)"
   timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --no-extras --steps 10 --cpu-seconds 3 \
