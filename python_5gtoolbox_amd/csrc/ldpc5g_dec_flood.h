@@ -39,6 +39,12 @@ constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 #define LDPC5G_FLOOD_ASB 0
 #endif
 constexpr int kAPre = LDPC5G_FLOOD_APRE;
+// phase B: edge k's sign bit by one shift of the row's sign word (u << k) per edge it adds, instead
+// of shifting the word once per edge of the row (the LDS rows' halves add alternate edges)
+#ifndef LDPC5G_FLOOD_BSHIFT
+#define LDPC5G_FLOOD_BSHIFT 0
+#endif
+constexpr bool kBShift = LDPC5G_FLOOD_BSHIFT != 0;
 constexpr bool kASb = LDPC5G_FLOOD_ASB != 0;
 
 // Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
@@ -578,7 +584,7 @@ __device__ __forceinline__ void flood_body(
                     return n;
                 }();
                 if constexpr (j < KC && (split < 0 || cidx % NP == split)) {
-                    const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
+                    const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), kBShift ? u << k : u, mv);
                     lds_T& acc = at(j * CS * TS + rot(gshift(e0 + k)));
                     if constexpr (kFloodPlan<BG, T, NP, CS>.first_row[j] == i) {
                         acc = T(0) + r;
@@ -592,7 +598,7 @@ __device__ __forceinline__ void flood_body(
                         acc = acc + r;
                     }
                 }
-                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
+                if constexpr (!kBShift) asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
             });
         };
         // the core LLRs of the LQ update, loaded now so phase B hides their latency

@@ -47,6 +47,8 @@ FLAGS = {
     "pre1sb": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=1"],
     "pre2sb": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=1"],
     "pre3sb": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=1"],
+    "bshift": ["-DLDPC5G_FLOOD_BSHIFT=1"],
+    "pre2bs": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_BSHIFT=1"],
 }
 for _n in FLAGS:
     VARIANTS.setdefault(_n, [])
