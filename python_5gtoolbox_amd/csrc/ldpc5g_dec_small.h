@@ -35,7 +35,7 @@ constexpr int small_cpt() { return RPT == 1 ? 1 : 2; }
 template <int BG>
 struct SmallPlan {
     int16_t cstart[BGT<BG>::KC + 1] = {};
-    uint16_t ew[BGT<BG>::E] = {};   // static part of an edge word: column | CSC position << 8
+    uint32_t ew[BGT<BG>::E] = {};   // static part of an edge word: column | CSC position << 8
     int ncore = 0, dmax = 0;
     constexpr SmallPlan() {
         using P = BGT<BG>;
@@ -44,12 +44,12 @@ struct SmallPlan {
             cstart[j] = (int16_t)n;
             for (int i = 0; i < P::MB; ++i)
                 for (int e = P::RS[i]; e < P::RS[i + 1]; ++e)
-                    if (P::COL[e] == j) ew[e] = (uint16_t)(j | (n++ << 8));
+                    if (P::COL[e] == j) ew[e] = (uint32_t)(j | (n++ << 8));
         }
         cstart[P::KC] = (int16_t)n;
         ncore = n;
         for (int e = 0; e < P::E; ++e)
-            if (P::COL[e] >= P::KC) ew[e] = (uint16_t)P::COL[e];
+            if (P::COL[e] >= P::KC) ew[e] = (uint32_t)P::COL[e];
         for (int i = 0; i < P::MB; ++i) dmax = dmax > P::RS[i + 1] - P::RS[i] ? dmax : P::RS[i + 1] - P::RS[i];
     }
 };
@@ -58,27 +58,35 @@ __device__ constexpr SmallPlan<BG> kSmallPlanD{};
 template <int BG>
 constexpr SmallPlan<BG> kSmallPlanH{};
 
+// LDS bytes: LQ twice per core column (entries z and z + Zc hold LQ of row z, so a read at z + V
+// mod Zc needs no wrap), one message per core edge, two edge words per edge, flags
 template <int BG, typename T>
 constexpr size_t small_lds_bytes_t(int Zc) {
     using P = BGT<BG>;
-    return (size_t)(P::KC + kSmallPlanH<BG>.ncore) * Zc * sizeof(T) + (size_t)(P::E + 4) * 4;
+    return (size_t)(2 * P::KC + kSmallPlanH<BG>.ncore) * Zc * sizeof(T) + (size_t)(2 * P::E + 4) * 4;
 }
 
-template <int BG, typename T, bool OFS, int kSmallRpt>
+template <int BG, typename T, bool OFS, int RPT>
 __global__ __launch_bounds__(kSmallMaxThreads) void ldpc_small_kernel(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int Zc, int zi, int64_t ldl, int64_t ldc, int L, T alpha, T beta,
     int pc) {
     using P = BGT<BG>;
-    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, E = P::E;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, E = P::E, TS = sizeof(T);
     constexpr int NCE = kSmallPlanH<BG>.ncore, DMAX = kSmallPlanH<BG>.dmax;
-    constexpr int CH = 8;   // edges whose LQ reads are in flight together
-    constexpr int kSmallCpt = small_cpt<kSmallRpt>();
+    constexpr int CPT = small_cpt<RPT>();
+    constexpr int CH = 10;   // LQ reads in flight together (BG2's widest row; BG1's rows 0-3 in two)
     extern __shared__ __align__(16) unsigned char smem[];
-    T* LQ = (T*)smem;                           // [KC][Zc]  LQ of the core columns
-    T* LR = LQ + KC * Zc;                       // [NCE][Zc] message at CSC position p, column row z'
-    uint32_t* ew = (uint32_t*)(LR + NCE * Zc);  // [E] column | CSC position << 8 | (V mod Zc) << 20
-    int* flag = (int*)(ew + E);                 // "some row failed" epoch, then the final verdict
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
+    using lds_T = __attribute__((address_space(3))) T;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    auto at = [&](uint32_t byte) -> lds_T& { return *(lds_T*)(uintptr_t)byte; };
+    auto word = [&](uint32_t byte) -> lds_u32& { return *(lds_u32*)(uintptr_t)byte; };
+    const uint32_t ZT = (uint32_t)(Zc * TS);
+    // byte offsets: LQ2 [KC][2 Zc] | LR [NCE][Zc] | read words [E] | write words [E] | flags
+    const uint32_t LR_B = 2u * KC * ZT, RW_B = LR_B + (uint32_t)NCE * ZT, WW_B = RW_B + 4u * E;
+    const uint32_t FL_B = WW_B + 4u * E;
 
     const int cb = blockIdx.x;
     const T* lrow = llr + (int64_t)cb * ldl;
@@ -86,47 +94,53 @@ __global__ __launch_bounds__(kSmallMaxThreads) void ldpc_small_kernel(
     const int t = threadIdx.x, NT = blockDim.x;
     const int NR = MB * Zc, NC = KC * Zc;
 
-    // ---- edge words (one thread per edge: a single round trip to the constant tables); LQ =
-    //      LLRin (:94), punctured columns 0 (:43)
-    for (int e = t; e < E; e += NT)
-        ew[e] = (uint32_t)kSmallPlanD<BG>.ew[e] | ((uint32_t)shift_of<BG>(zi, e) << 20);
-    if (t == 0) flag[0] = 0, flag[1] = 0;
-    // own core column entries c = j*Zc + z': channel LLR and CSC range stay in registers
-    T lf[kSmallCpt];
-    int cz[kSmallCpt], cp0[kSmallCpt], cp1[kSmallCpt];
-    bool cpun[kSmallCpt];
+    // ---- edge words, one thread per edge (a single round trip to the constant tables): read word
+    //      = byte offset of LQ2 entry (column j, row V mod Zc) relative to row z; write word = byte
+    //      offset of the edge's message slot (CSC position p) | (V mod Zc) * TS << 18
+    for (int e = t; e < E; e += NT) {
+        const uint32_t w0 = kSmallPlanD<BG>.ew[e];
+        const uint32_t j = w0 & 0xffu, pp = w0 >> 8;
+        const uint32_t sb = (uint32_t)shift_of<BG>(zi, e) * TS;
+        const bool core = j < (uint32_t)KC;
+        word(RW_B + 4u * e) = core ? 2u * j * ZT + sb : 0u;
+        word(WW_B + 4u * e) = core ? (LR_B + pp * ZT) | (sb << 18) : 0u;
+    }
+    if (t == 0) word(FL_B) = 0u, word(FL_B + 4) = 0u;
+    // own core column entries c = j*Zc + z': LLR, CSC range, LQ2 / message byte offsets
+    T lf[CPT];
+    uint32_t cq[CPT], cr[CPT];
+    int cn[CPT];
+    bool cpun[CPT];
 #pragma unroll
-    for (int k = 0; k < kSmallCpt; ++k) {
+    for (int k = 0; k < CPT; ++k) {
         const int c = t + k * NT;
-        const int j = c < NC ? c / Zc : 0;
-        cz[k] = c - j * Zc;
-        cp0[k] = kSmallPlanD<BG>.cstart[j], cp1[k] = kSmallPlanD<BG>.cstart[j + 1];
+        const int j = c < NC ? c / Zc : 0, z = c - j * Zc;
+        const int p0 = kSmallPlanD<BG>.cstart[j];
+        cn[k] = kSmallPlanD<BG>.cstart[j + 1] - p0;
+        cq[k] = 2u * (uint32_t)j * ZT + (uint32_t)z * TS;
+        cr[k] = LR_B + (uint32_t)p0 * ZT + (uint32_t)z * TS;
         cpun[k] = j < pc;
-        lf[k] = (c < NC && j >= pc) ? lrow[(j - pc) * Zc + cz[k]] : T(0);
-        if (c < NC) LQ[c] = lf[k];
+        lf[k] = (c < NC && j >= pc) ? lrow[(j - pc) * Zc + z] : T(0);
+        if (c < NC) at(cq[k]) = lf[k], at(cq[k] + ZT) = lf[k];
     }
     // own check nodes r = i*Zc + z: row state (nA, nB, signs | argmin << 24), extension LLR
-    T nA[kSmallRpt], nB[kSmallRpt], xl[kSmallRpt];
-    uint32_t wd[kSmallRpt];
-    int ri[kSmallRpt], rz[kSmallRpt], re0[kSmallRpt], rd[kSmallRpt];
+    T nA[RPT], nB[RPT], xl[RPT];
+    uint32_t wd[RPT], zb[RPT];
+    int ri[RPT], re0[RPT], rd[RPT];
 #pragma unroll
-    for (int k = 0; k < kSmallRpt; ++k) {
+    for (int k = 0; k < RPT; ++k) {
         const int r = t + k * NT;
         ri[k] = r < NR ? r / Zc : 0;
-        rz[k] = r - ri[k] * Zc;
+        const int z = r - ri[k] * Zc;
+        zb[k] = (uint32_t)z * TS;
         re0[k] = row_start_d<BG>(ri[k]);
         rd[k] = row_start_d<BG>(ri[k] + 1) - re0[k];
         nA[k] = T(0), nB[k] = T(0), wd[k] = 0u;
-        xl[k] = (r < NR && ri[k] >= 4) ? lrow[(KB + ri[k] - pc) * Zc + rz[k]] : T(0);
+        xl[k] = (r < NR && ri[k] >= 4) ? lrow[(KB + ri[k] - pc) * Zc + z] : T(0);
     }
     lds_barrier();
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR v_bitop3 is full rate)
     asm volatile("" : "+v"(mv));
-    // entry (z + s) mod Zc of a column
-    auto rot = [&](int z, uint32_t s) -> int {
-        const int zz = z + (int)s;
-        return zz >= Zc ? zz - Zc : zz;
-    };
 
     uint32_t hdx = 0;   // bit k: extension decision of own node k (LQ_old < 0) in the last phase A
     int it = 0;
@@ -136,48 +150,50 @@ __global__ __launch_bounds__(kSmallMaxThreads) void ldpc_small_kernel(
         bool fail = false;
         hdx = 0;
 #pragma unroll
-        for (int k = 0; k < kSmallRpt; ++k) {
+        for (int k = 0; k < RPT; ++k) {
             if (t + k * NT >= NR) continue;
-            const int z = rz[k], e0 = re0[k], d = rd[k];
-            // the row's edge words, all requested at once (LDS broadcast within a row)
+            const int e0 = re0[k], d = rd[k];
+            const bool xe = ri[k] >= 4;         // rows >= 4: the last edge is the extension column
+            const int dc = d - (xe ? 1 : 0);    // core edges
+            // the row's LQ reads, all in flight before the first is used (read words are LDS
+            // broadcasts within a row)
             uint32_t W[DMAX];
 #pragma unroll
-            for (int x = 0; x < DMAX; ++x) W[x] = x < d ? ew[e0 + x] : (uint32_t)KC;
+            for (int x = 0; x < DMAX; ++x) W[x] = word(RW_B + 4u * (uint32_t)(e0 + (x < dc ? x : 0)));
             uint32_t u = wd[k] << (32 - d);
             const uint32_t idxo = wd[k] >> 24;
             const T mA = nA[k], mB = nB[k];
             T min1 = FT<T>::inf(), min2 = FT<T>::inf();
             uint32_t sx = 0, idx = 0, negs = 0;
             bool par = false;
-#pragma unroll
-            for (int c0 = 0; c0 < DMAX; c0 += CH) {
+            auto edge = [&](int q0, T av, T rold) {
+                par ^= av < T(0);
+                const T q = av - rold;
+                const T aq = fabs(q);
+                idx = aq < min1 ? (uint32_t)q0 : idx;
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                two_min(min1, min2, aq);
+                sx ^= FT<T>::sbits(q);
+            };
+            // LQ reads in chunks of CH, all of a chunk in flight before the first is used
+            sfor<0, (DMAX + CH - 1) / CH>([&](auto cc) {
+                constexpr int c0 = decltype(cc)::value * CH, c1 = c0 + CH < DMAX ? c0 + CH : DMAX;
                 T a[CH];
-#pragma unroll
-                for (int x = 0; x < CH && c0 + x < DMAX; ++x) {
-                    const uint32_t w = W[c0 + x];
-                    const int j = (int)(w & 0xffu);
-                    a[x] = LQ[(j < KC ? j : 0) * Zc + rot(z, w >> 20)];
-                }
-#pragma unroll
-                for (int x = 0; x < CH && c0 + x < DMAX; ++x) {
-                    const int q0 = c0 + x;
-                    if (q0 >= d) break;
-                    const int j = (int)(W[q0] & 0xffu);
-                    const T rold = xsign_v(idxo == (uint32_t)q0 ? mB : mA, u, mv);
-                    u <<= 1;
-                    T av = a[x];
-                    if (j >= KC) {
-                        av = xl[k] + rold;   // LQ of a degree-1 column = LLR + its only r
-                        hdx |= (uint32_t)(av < T(0)) << k;
+                sfor<c0, c1>([&](auto xc) { a[decltype(xc)::value - c0] = at(W[decltype(xc)::value] + zb[k]); });
+                sfor<c0, c1>([&](auto xc) {
+                    constexpr int q0 = decltype(xc)::value;
+                    if (q0 < dc) {
+                        const T rold = xsign_v(idxo == (uint32_t)q0 ? mB : mA, u, mv);
+                        u <<= 1;
+                        edge(q0, a[q0 - c0], rold);
                     }
-                    par ^= av < T(0);
-                    const T q = av - rold;
-                    const T aq = fabs(q);
-                    idx = aq < min1 ? (uint32_t)q0 : idx;
-                    negs = (negs << 1) | (FT<T>::sbits(q) >> 31);
-                    two_min(min1, min2, aq);
-                    sx ^= FT<T>::sbits(q);
-                }
+                });
+            });
+            if (xe) {   // LQ of the degree-1 column = LLR + its only r
+                const T rold = xsign_v(idxo == (uint32_t)dc ? mB : mA, u, mv);
+                const T av = xl[k] + rold;
+                hdx |= (uint32_t)(av < T(0)) << k;
+                edge(dc, av, rold);
             }
             fail |= par;
             T x1 = min1, x2 = min2;
@@ -189,50 +205,58 @@ __global__ __launch_bounds__(kSmallMaxThreads) void ldpc_small_kernel(
             const T nAk = alpha * x1, nBk = alpha * x2;
             nA[k] = nAk, nB[k] = nBk;
             wd[k] = (negs ^ flip) | (idx << 24);
-            // the new messages of the core edges, at their CSC position and column row
+            // the new messages of the core edges into their slots, at row (z + V) mod Zc
             uint32_t un = wd[k] << (32 - d);
+            uint32_t V[DMAX];
 #pragma unroll
-            for (int q0 = 0; q0 < DMAX; ++q0) {
-                if (q0 >= d) break;
-                const uint32_t w = W[q0];
-                if ((int)(w & 0xffu) < KC) {
+            for (int x = 0; x < DMAX; ++x) V[x] = word(WW_B + 4u * (uint32_t)(e0 + (x < dc ? x : 0)));
+            sfor<0, DMAX>([&](auto xc) {
+                constexpr int q0 = decltype(xc)::value;
+                if (q0 < dc) {
                     const T r = xsign_v(idx == (uint32_t)q0 ? nBk : nAk, un, mv);
-                    LR[(int)((w >> 8) & 0xfffu) * Zc + rot(z, w >> 20)] = r;
+                    un <<= 1;
+                    const uint32_t zz = zb[k] + (V[q0] >> 18);
+                    at((V[q0] & 0x3ffffu) + min(zz, zz - ZT)) = r;
                 }
-                un <<= 1;
-            }
+            });
         }
-        if (fail) flag[0] = it + 1;
+        if (fail) word(FL_B) = (uint32_t)(it + 1);
         lds_barrier();
-        if (flag[0] != it + 1) {
+        if (word(FL_B) != (uint32_t)(it + 1)) {
             // ---- the syndrome of LQ_old holds (:112-114): its hard decisions are the output
 #pragma unroll
-            for (int k = 0; k < kSmallCpt; ++k)
-                if (t + k * NT < NC) crow[t + k * NT] = (int8_t)(LQ[t + k * NT] < T(0));
+            for (int k = 0; k < CPT; ++k)
+                if (t + k * NT < NC) crow[t + k * NT] = (int8_t)(at(cq[k]) < T(0));
 #pragma unroll
-            for (int k = 0; k < kSmallRpt; ++k)
-                if (t + k * NT < NR && ri[k] >= 4) crow[(KB + ri[k]) * Zc + rz[k]] = (int8_t)((hdx >> k) & 1u);
+            for (int k = 0; k < RPT; ++k)
+                if (t + k * NT < NR && ri[k] >= 4)
+                    crow[(KB + ri[k]) * Zc + (int)(zb[k] / TS)] = (int8_t)((hdx >> k) & 1u);
             if (t == 0) status[cb] = 1, iters[cb] = it;
             return;
         }
         // ---- LQ = LLRin + Lr.sum(axis=0) (:126): core columns, rows ascending (consecutive
-        //      CSC slots, four reads in flight)
+        //      message slots, four reads in flight)
 #pragma unroll
-        for (int k = 0; k < kSmallCpt; ++k) {
+        for (int k = 0; k < CPT; ++k) {
             if (t + k * NT >= NC) continue;
-            const int z = cz[k], p1 = cp1[k];
-            int p = cp0[k];
-            T acc = T(0) + LR[p * Zc + z];
-            for (++p; p + 4 <= p1; p += 4) {
-                const T v0 = LR[p * Zc + z], v1 = LR[(p + 1) * Zc + z];
-                const T v2 = LR[(p + 2) * Zc + z], v3 = LR[(p + 3) * Zc + z];
+            const int n = cn[k];
+            uint32_t o = cr[k];
+            T acc = T(0) + at(o);
+            int p = 1;
+            for (; p + 4 <= n; p += 4) {
+                const T v0 = at(o + ZT), v1 = at(o + 2 * ZT), v2 = at(o + 3 * ZT), v3 = at(o + 4 * ZT);
+                o += 4 * ZT;
                 acc = acc + v0;
                 acc = acc + v1;
                 acc = acc + v2;
                 acc = acc + v3;
             }
-            for (; p < p1; ++p) acc = acc + LR[p * Zc + z];
-            LQ[t + k * NT] = (cpun[k] ? T(0) : lf[k]) + acc;   // punctured columns: LLR 0 (:43)
+            for (; p < n; ++p) {
+                o += ZT;
+                acc = acc + at(o);
+            }
+            const T v = (cpun[k] ? T(0) : lf[k]) + acc;   // punctured columns: LLR 0 (:43)
+            at(cq[k]) = v, at(cq[k] + ZT) = v;
         }
         lds_barrier();
     }
@@ -241,35 +265,37 @@ __global__ __launch_bounds__(kSmallMaxThreads) void ldpc_small_kernel(
     bool fail = false;
     uint32_t ox = 0;
 #pragma unroll
-    for (int k = 0; k < kSmallRpt; ++k) {
+    for (int k = 0; k < RPT; ++k) {
         if (t + k * NT >= NR) continue;
-        const int i = ri[k], z = rz[k], e0 = re0[k], d = rd[k];
+        const int e0 = re0[k], d = rd[k];
+        const bool xe = ri[k] >= 4;
+        const int dc = d - (xe ? 1 : 0);
         bool par = false;
-        if (i >= 4) {   // the extension edge is the row's last: LLR + its r
-            const T rx = xsign_v((wd[k] >> 24) == (uint32_t)(d - 1) ? nB[k] : nA[k], wd[k] << 31, mv);
+        if (xe) {   // the extension edge is the row's last: LLR + its r
+            const T rx = xsign_v((wd[k] >> 24) == (uint32_t)dc ? nB[k] : nA[k], wd[k] << 31, mv);
             const bool b = xl[k] + rx <= T(0);
             ox |= (uint32_t)b << k;
             par = b;
         }
         uint32_t W[DMAX];
 #pragma unroll
-        for (int x = 0; x < DMAX; ++x) W[x] = x < d ? ew[e0 + x] : (uint32_t)KC;
-#pragma unroll
-        for (int x = 0; x < DMAX; ++x) {
-            const int j = (int)(W[x] & 0xffu);
-            if (j < KC) par ^= LQ[j * Zc + rot(z, W[x] >> 20)] <= T(0);
-        }
+        for (int x = 0; x < DMAX; ++x) W[x] = word(RW_B + 4u * (uint32_t)(e0 + (x < dc ? x : 0)));
+        sfor<0, DMAX>([&](auto xc) {
+            constexpr int x = decltype(xc)::value;
+            const bool b = at(W[x] + zb[k]) <= T(0);
+            par ^= x < dc && b;
+        });
         fail |= par;
     }
-    if (fail) flag[1] = 1;
+    if (fail) word(FL_B + 4) = 1u;
     lds_barrier();
 #pragma unroll
-    for (int k = 0; k < kSmallCpt; ++k)
-        if (t + k * NT < NC) crow[t + k * NT] = (int8_t)(LQ[t + k * NT] <= T(0));
+    for (int k = 0; k < CPT; ++k)
+        if (t + k * NT < NC) crow[t + k * NT] = (int8_t)(at(cq[k]) <= T(0));
 #pragma unroll
-    for (int k = 0; k < kSmallRpt; ++k)
-        if (t + k * NT < NR && ri[k] >= 4) crow[(KB + ri[k]) * Zc + rz[k]] = (int8_t)((ox >> k) & 1u);
-    if (t == 0) status[cb] = flag[1] == 0, iters[cb] = L;
+    for (int k = 0; k < RPT; ++k)
+        if (t + k * NT < NR && ri[k] >= 4) crow[(KB + ri[k]) * Zc + (int)(zb[k] / TS)] = (int8_t)((ox >> k) & 1u);
+    if (t == 0) status[cb] = word(FL_B + 4) == 0u, iters[cb] = L;
 }
 
 template <int BG, typename T, bool OFS, int RPT>
@@ -286,7 +312,7 @@ int launch_small_rpt(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
                      hipStream_t st) {
     const bool ofs = beta != 0.0;
     auto kern = ofs ? ldpc_small_kernel<BG, T, true, RPT> : ldpc_small_kernel<BG, T, false, RPT>;
-    const size_t lds = small_lds_bytes_t<BG, T>(64);   // one attribute value for every Zc <= 64
+    const size_t lds = kLdsPerCU;   // one attribute value for every Zc (the launch asks for what it needs)
     if (int rc = ofs ? set_lds_once<small_kernel<BG, T, true, RPT>()>(lds) : set_lds_once<small_kernel<BG, T, false, RPT>()>(lds))
         return rc;
     const size_t lds_zc = small_lds_bytes_t<BG, T>(Zc);
