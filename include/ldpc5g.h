@@ -79,6 +79,21 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
                      double alpha, double beta, int32_t schedule, int32_t flags, int64_t ldl,
                      int64_t ldc, void* stream);
 
+/* Per-codeblock drop-in shape, HOST buffers in and out  <- py5gphy/ldpc/nr_ldpc_decode.py:11-49
+ * nr_decode_ldpc(LLRin, Zc, bgn, L, 'min-sum', alpha, beta) and nr_ldpc_encode.py:8 encode_ldpc(ck,
+ * bgn), called one codeblock at a time by the reference's callers (nr_dlsch_decode.py:91,
+ * scripts/internal/sim_ldpc_internal.py:50-58).  float64 flooding min-sum (bit-exact with the
+ * reference) / the encoder on B contiguous host rows (llr [B][N or Nf], ck [B][Nf], status [B],
+ * iters [B]; ck [B][K], dn [B][N]): the rows go through a per-thread pinned staging buffer and a
+ * per-thread device buffer (grown on demand and held for the life of the process), one H2D copy,
+ * the kernel, one D2H copy and one synchronisation of `stream` — no caller-side device memory.
+ * Synchronous: returns when the outputs are written.  beta < 0 is rejected (see decode_sparse). */
+int ldpc5g_decode_ms_host(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                          int32_t B, int32_t bgn, int32_t Zc, int32_t L, double alpha, double beta,
+                          int32_t flags, void* stream);
+int ldpc5g_encode_host(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t Zc,
+                       void* stream);
+
 /* Hard-decision bit flipping (algo='BF')  <- py5gphy/ldpc/ldpc_decoder_bit_flipping.py:5-73
  * reached through nr_decode_ldpc(..., algo='BF') (nr_ldpc_decode.py:65-67).  Same buffers as
  * ldpc5g_decode_ms; ck holds the 0/1 decisions (the reference returns them as float64), status

@@ -32,6 +32,11 @@ SIGNATURES = {
                                     _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32, _c.c_double,
                                     _c.c_double, _c.c_int32, _c.c_int32, _c.c_int64, _c.c_int64,
                                     _c.c_void_p]),
+    "ldpc5g_decode_ms_host": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                         _c.c_int32, _c.c_int32, _c.c_int32, _c.c_int32,
+                                         _c.c_double, _c.c_double, _c.c_int32, _c.c_void_p]),
+    "ldpc5g_encode_host": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int32, _c.c_int32, _c.c_int32,
+                                      _c.c_void_p]),
     "ldpc5g_decode_ms_mixed": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_int32,
                                           _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
                                           _c.c_double, _c.c_double, _c.c_int32, _c.c_int32,

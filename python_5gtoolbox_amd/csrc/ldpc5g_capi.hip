@@ -254,6 +254,99 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
                       ldl, ldc, L, alpha, beta, pc, (flags & LDPC5G_RATE_MATCHED) != 0, (hipStream_t)stream);
 }
 
+namespace ldpc5g_impl {
+namespace {
+// Per-thread device + pinned buffers of the host-buffer entry points (grown on demand, never freed:
+// a thread-exit destructor could run after the HIP runtime is gone; include/ldpc5g.h states it).
+struct HostStage {
+    void* dev = nullptr;
+    size_t dcap = 0;
+    void* pin = nullptr;
+    size_t pcap = 0;
+    int device = -1;
+};
+thread_local HostStage t_hs;
+
+int host_stage(size_t bytes, unsigned char** d, unsigned char** p) {
+    int dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    HostStage& h = t_hs;
+    if (h.device != dev) h = HostStage{}, h.device = dev;   // buffers of another device stay alive
+    if (h.dcap < bytes) {
+        if (h.dev) (void)hipFree(h.dev);
+        h.dev = nullptr, h.dcap = 0;
+        if (int rc = check_hip(hipMalloc(&h.dev, bytes), "hipMalloc(host stage)")) return rc;
+        h.dcap = bytes;
+    }
+    if (h.pcap < bytes) {
+        if (h.pin) (void)hipHostFree(h.pin);
+        h.pin = nullptr, h.pcap = 0;
+        if (int rc = check_hip(hipHostMalloc(&h.pin, bytes, hipHostMallocDefault), "hipHostMalloc(host stage)")) return rc;
+        h.pcap = bytes;
+    }
+    *d = (unsigned char*)h.dev, *p = (unsigned char*)h.pin;
+    return LDPC5G_OK;
+}
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+}  // namespace
+}  // namespace ldpc5g_impl
+
+int ldpc5g_decode_ms_host(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int32_t B,
+                          int32_t bgn, int32_t Zc, int32_t L, double alpha, double beta, int32_t flags,
+                          void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int pc = (flags & LDPC5G_LLR_FULL) ? 0 : 2;
+    const int N = (bgn == 1 ? 66 : 50) * Zc + (2 - pc) * Zc, Nf = (bgn == 1 ? 68 : 52) * Zc;
+    if (B < 0 || L < 0) return fail(LDPC5G_ESIZE, "bad sizes B=%d L=%d", B, L);
+    if (!(beta >= 0.0)) return fail(LDPC5G_ESIZE, "beta=%g: the offset must be >= 0 (nr_ldpc_decode.py:60)", beta);
+    if (B == 0) return LDPC5G_OK;
+    if (!llr || !ck || !status || !iters) return fail(LDPC5G_ESIZE, "null buffer");
+    const size_t nin = (size_t)B * N * sizeof(double), nck = (size_t)B * Nf;
+    const size_t o_ck = align16(nin), o_st = align16(o_ck + nck), o_it = align16(o_st + B);
+    const size_t total = o_it + (size_t)B * 4;
+    unsigned char *d = nullptr, *p = nullptr;
+    if (int rc = host_stage(total, &d, &p)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    memcpy(p, llr, nin);
+    if (int rc = check_hip(hipMemcpyAsync(d, p, nin, hipMemcpyHostToDevice, st), "hipMemcpyAsync(llr)")) return rc;
+    if (int rc = launch_dec(bgn, LDPC5G_F64, false, d, (int8_t*)(d + o_ck), d + o_st, (int32_t*)(d + o_it), B, Zc, zi,
+                            N, Nf, L, alpha, beta, pc, (flags & LDPC5G_RATE_MATCHED) != 0, st))
+        return rc;
+    if (int rc = check_hip(hipMemcpyAsync(p + o_ck, d + o_ck, total - o_ck, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(out)"))
+        return rc;
+    if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize")) return rc;
+    memcpy(ck, p + o_ck, nck);
+    memcpy(status, p + o_st, (size_t)B);
+    memcpy(iters, p + o_it, (size_t)B * 4);
+    return LDPC5G_OK;
+}
+
+int ldpc5g_encode_host(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t Zc, void* stream) {
+    g_err.clear();
+    if (bgn != 1 && bgn != 2) return fail(LDPC5G_EBGN, "bgn must be 1 or 2 (got %d)", bgn);
+    const int zi = zc_index(Zc);
+    if (zi < 0) return fail(LDPC5G_EZC, "Zc=%d is not a TS 38.212 lifting size", Zc);
+    const int K = (bgn == 1 ? 22 : 10) * Zc, N = (bgn == 1 ? 66 : 50) * Zc;
+    if (B < 0) return fail(LDPC5G_ESIZE, "bad size B=%d", B);
+    if (B == 0) return LDPC5G_OK;
+    if (!ck || !dn) return fail(LDPC5G_ESIZE, "null buffer");
+    const size_t nk = (size_t)B * K, o_dn = align16(nk), total = o_dn + (size_t)B * N;
+    unsigned char *d = nullptr, *p = nullptr;
+    if (int rc = host_stage(total, &d, &p)) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    memcpy(p, ck, nk);
+    if (int rc = check_hip(hipMemcpyAsync(d, p, nk, hipMemcpyHostToDevice, st), "hipMemcpyAsync(ck)")) return rc;
+    if (int rc = launch_encode((const int8_t*)d, (int8_t*)(d + o_dn), B, bgn, Zc, zi, K, N, st)) return rc;
+    if (int rc = check_hip(hipMemcpyAsync(p + o_dn, d + o_dn, (size_t)B * N, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(dn)"))
+        return rc;
+    if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize")) return rc;
+    memcpy(dn, p + o_dn, (size_t)B * N);
+    return LDPC5G_OK;
+}
+
 int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
                      int32_t* iters, int32_t B, int32_t bgn, int32_t Zc, int32_t L, int32_t flags,
                      int64_t ldl, int64_t ldc, void* stream) {

@@ -708,17 +708,18 @@ __device__ __forceinline__ void dec_body(
             }
         });
 
+        const int clq = valid ? t - zv * G : 0;
         {
             // ---- layered stopping rule: no hard decision changed over the iteration, then an
             //      exact syndrome check of those decisions (oracle.decode_layered)
             uint32_t hdc = 0;
             if (active)
                 for (int j = 0; j < KC; ++j) hdc |= (uint32_t)(own(j) < T(0)) << j;
-            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[cl] = 1;
+            if (active && (hdc != hdc_prev || hdx != hdx_prev)) flagA[clq] = 1;
             // a stopped slot keeps the decisions of its stopping iteration (staged at the end)
             if (active) hdc_prev = hdc, hdx_prev = hdx;
             lds_barrier();
-            const bool cand = active && flagA[cl] == 0;
+            const bool cand = active && flagA[clq] == 0;
             if (block_any(cand)) {
                 if (cand) {
                     const bool sf = syndrome_fails<BG, all_rows<BG>(), true, T, false>(
@@ -727,17 +728,23 @@ __device__ __forceinline__ void dec_body(
                             return at(P::COL[e] * CS * TS + rot(shift_of<BG>(ziv, e)));
                         },
                         [&](auto ic) -> bool { return (hdx >> (decltype(ic)::value - 4)) & 1u; });
-                    if (sf) flagB[cl] = 1;
+                    if (sf) flagB[clq] = 1;
                 }
                 lds_barrier();
-                if (cand && flagB[cl] == 0) {
-                    if (z == 0) status[out] = 1, iters[out] = it + 1;
+                if (cand && flagB[clq] == 0) {
+                    if (z == 0) {
+                        int tq = t;
+                        asm volatile("" : "+v"(tq));
+                        const int cq = tq - zv * G;
+                        const int oq = work ? cbs[work[blockIdx.x].first + cq].out : (int)blockIdx.x * G + cq;
+                        status[oq] = 1, iters[oq] = it + 1;
+                    }
                     active = false;
                 }
             }
         }
         lds_barrier();
-        if (z == 0 && valid) flagA[cl] = 0, flagB[cl] = 0;
+        if (z == 0 && valid) flagA[clq] = 0, flagB[clq] = 0;
         if (!block_any(active)) break;
     }
 
@@ -757,6 +764,20 @@ __device__ __forceinline__ void dec_body(
     };
     zv = z;
     asm volatile("" : "+v"(zv));   // keep the output addresses out of the loop (no hoist/spill)
+    int t2 = t;
+    asm volatile("" : "+v"(t2));
+    const int cl2 = t2 - zv * G;   // zv = z here (no division)
+    int out2 = 0;
+    const T* lrow2 = llr;
+    if (valid) {
+        if (work) {
+            const CbRef r2 = cbs[work[blockIdx.x].first + cl2];
+            out2 = r2.out, lrow2 = llr + r2.llr_off;
+        } else {
+            out2 = (int)blockIdx.x * G + cl2, lrow2 = llr + (int64_t)out2 * ldl;
+        }
+    }
+    auto llrx2 = [&](int i4) -> T { return lrow2[(KB + 4 + i4 - pc) * Zc + zv]; };
     if (active) {
         // extension decisions first, their LLRs requested in batches of 14 before any is used (one
         // load per row made the scheduler serialise them; all 42 at once spill), so the row state
@@ -766,7 +787,7 @@ __device__ __forceinline__ void dec_body(
         sfor<0, (NX + XB - 1) / XB>([&](auto bc) {
             constexpr int x0 = decltype(bc)::value * XB, x1 = x0 + XB < NX ? x0 + XB : NX;
             T vx[XB];
-            sfor<x0, x1>([&](auto xc) { vx[decltype(xc)::value - x0] = llrx(decltype(xc)::value); });
+            sfor<x0, x1>([&](auto xc) { vx[decltype(xc)::value - x0] = llrx2(decltype(xc)::value); });
             __builtin_amdgcn_sched_barrier(0);
             sfor<x0, x1>([&](auto xc) {
                 constexpr int i = decltype(xc)::value + 4;
@@ -780,27 +801,29 @@ __device__ __forceinline__ void dec_body(
                 return at(P::COL[e] * CS * TS + rot_v(shift_of<BG>(zi, e)));
             },
             [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
-        if (fail) flagA[cl] = 1;
+        if (fail) flagA[cl2] = 1;
         uint32_t oc = 0;
         for (int j = 0; j < KC; ++j) oc |= (uint32_t)(own(j) <= T(0)) << j;
         hdc_prev = oc, hdx_prev = ox;
     }
     lds_barrier();   // every APP / state read is done: LDS below FLAG_B is free from here
     if (active && z == 0) {
-        status[out] = flagA[cl] == 0;
-        iters[out] = L;
+        status[out2] = flagA[cl2] == 0;
+        iters[out2] = L;
     }
     // ---- ck through LDS (ck_store_staged): LDS below FLAG_B is free, and G * SS <= 768 * Nf + 15 * G
     //      fits it for every Zc
     {
         const int NFZ = P::NB * Zc;
         if (valid) {
-            const uint32_t sb = (uint32_t)(cl * ck_stage_stride(NFZ) + zv);
+            const uint32_t sb = (uint32_t)(cl2 * ck_stage_stride(NFZ) + zv);
             for (int j = 0; j < KC; ++j) ck_stage_byte(sb + (uint32_t)(j * Zc), (hdc_prev >> j) & 1u);
             for (int i4 = 0; i4 < MB - 4; ++i4)
                 ck_stage_byte(sb + (uint32_t)((KB + 4 + i4) * Zc), (uint32_t)(hdx_prev >> i4) & 1u);
         }
-        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow));   // orders the staging too
+        int8_t* crow2 = ck;
+        if (valid) crow2 = work ? ck + cbs[work[blockIdx.x].first + cl2].ck_off : ck + (int64_t)out2 * ldc;
+        const bool slow = block_any(valid && !ck_row_aligned(NFZ, crow2));   // orders the staging too
         const int nslots = work ? G : min(G, B - (int)blockIdx.x * G);
         ck_store_staged(NFZ, nslots, [&](int sl) -> int8_t* {
             if (work) return ck + cbs[work[blockIdx.x].first + sl].ck_off;

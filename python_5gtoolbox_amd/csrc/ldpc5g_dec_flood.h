@@ -31,12 +31,13 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 // extension-column LLRs are loaded this many ext rows ahead of their use in phase A
 constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 // phase A: core-edge LQ reads issued this many edges ahead (0: at their use), and whether a
-// scheduling barrier pins each read before the arithmetic of the edge it overlaps
+// scheduling barrier pins each read before the arithmetic of the edge it overlaps (r04: one edge
+// ahead + barrier 4.205 -> 4.041 ms per 4096 f64 codeblocks; 2 or 3 ahead 4.06 ms)
 #ifndef LDPC5G_FLOOD_APRE
-#define LDPC5G_FLOOD_APRE 0
+#define LDPC5G_FLOOD_APRE 1
 #endif
 #ifndef LDPC5G_FLOOD_ASB
-#define LDPC5G_FLOOD_ASB 0
+#define LDPC5G_FLOOD_ASB 1
 #endif
 constexpr int kAPre = LDPC5G_FLOOD_APRE;
 // phase B: edge k's sign bit by one shift of the row's sign word (u << k) per edge it adds, instead

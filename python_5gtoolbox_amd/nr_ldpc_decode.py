@@ -108,13 +108,27 @@ def nr_decode_ldpc_batch(LLR, Zc, bgn, L, algo="min-sum", alpha=1.0, beta=0.0,
 
 
 def _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, full):
-    """One codeblock through the float64 flooding kernel (the reference-exact path) with pinned
-    staging: LLRs -> pinned -> device, decode into one device record (ck | status | iters), one
-    D2H of that record.  Returns (ck int8 (Nf,), status bool)."""
+    """One codeblock through the float64 kernels (the reference-exact path).  min-sum: host
+    buffers straight through the library (ldpc5g_decode_ms_host: per-thread pinned / device
+    staging, one H2D, the launch, one D2H, one synchronisation); BF / BP through the batched
+    device path.  Returns (ck int8 (Nf,), status bool)."""
     t = _lib.require_gpu()
     K, N, Nf = code_dims(bgn, Zc)
-    n_in = Nf if full else N
+    x = np.ascontiguousarray(np.asarray(LLRin, np.float64).reshape(-1))
+    if algo == "min-sum":
+        ck = np.empty(Nf, np.int8)
+        st = np.zeros(1, np.uint8)
+        it = np.zeros(1, np.int32)
+        # a last parity column of exact +0.0 (untransmitted after rate recovery, e.g. DLSCHDecode's
+        # rows at high code rates) enables dead-row skipping: same results, less work
+        rm = not x[-Zc:].view(np.int64).any()
+        flags = (_lib.LLR_FULL if full else 0) | (_lib.RATE_MATCHED if rm else 0)
+        _lib.check(_lib.lib().ldpc5g_decode_ms_host(
+            x.ctypes.data, ck.ctypes.data, st.ctypes.data, it.ctypes.data, 1, bgn, Zc, int(L),
+            float(alpha), float(beta), flags, _lib.stream_ptr()))
+        return ck, bool(st[0])
     dev = t.cuda.current_device()
+    n_in = Nf if full else N
 
     def make():
         return (t.empty((1, n_in), dtype=t.float64, pin_memory=True),
@@ -122,15 +136,10 @@ def _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, full):
                 t.empty((Nf + 8,), dtype=t.uint8, device=dev),
                 t.empty((Nf + 8,), dtype=t.uint8, pin_memory=True))
     hin, din, drec, hrec = _lib.staging(("dec1", dev, n_in, Nf), make)
-    x = np.asarray(LLRin, np.float64).reshape(-1)
     hin.numpy()[0] = x
     din.copy_(hin, non_blocking=True)
     out = (drec[:Nf].view(t.int8).view(1, Nf), drec[Nf:Nf + 1], drec[Nf + 4:Nf + 8].view(t.int32))
-    # a last parity column of exact +0.0 (untransmitted after rate recovery, e.g. DLSCHDecode's
-    # rows at high code rates) enables dead-row skipping: same results, less work
-    rm = algo == "min-sum" and not x[-Zc:].view(np.int64).any()
-    nr_decode_ldpc_batch(din, Zc, bgn, L, algo, alpha, beta, "flooding", full=full, out=out,
-                         rate_matched=rm)
+    nr_decode_ldpc_batch(din, Zc, bgn, L, algo, alpha, beta, "flooding", full=full, out=out)
     hrec.copy_(drec, non_blocking=True)
     t.cuda.current_stream().synchronize()
     h = hrec.numpy()

@@ -61,19 +61,13 @@ def encode_ldpc(ck, bgn):
     Zc, N = _dims(K, bgn)
     iLS = find_iLS(Zc)
     assert iLS < 8
-    t = _lib.require_gpu()
-    dev = t.cuda.current_device()
-
-    def make():   # pinned staging (see _lib.staging): one H2D, the launch, one D2H per call
-        return (t.empty((1, K), dtype=t.int8, pin_memory=True), t.empty((1, K), dtype=t.int8, device=dev),
-                t.empty((1, N), dtype=t.int8, device=dev), t.empty((1, N), dtype=t.int8, pin_memory=True))
-    hin, din, dout, hout = _lib.staging(("enc1", dev, K, bgn), make)
-    hin.numpy()[0] = np.asarray(ck).reshape(-1)
-    din.copy_(hin, non_blocking=True)
-    encode_ldpc_batch(din, bgn, out=dout)
-    hout.copy_(dout, non_blocking=True)
-    t.cuda.current_stream().synchronize()
-    dn = hout.numpy()[0].copy()
+    _lib.require_gpu()
+    # host rows straight through the library (ldpc5g_encode_host: its per-thread pinned / device
+    # staging, one H2D, the launch, one D2H, one synchronisation — no torch op on the way)
+    x = np.ascontiguousarray(np.asarray(ck).reshape(-1), dtype=np.int8)
+    dn = np.empty(N, np.int8)
+    _lib.check(_lib.lib().ldpc5g_encode_host(x.ctypes.data, dn.ctypes.data, 1, bgn, Zc,
+                                             _lib.stream_ptr()))
     # reference side effect: fillers of the caller's block are zeroed in place (:34-35)
     tail = ck[2 * Zc:K]
     tail[tail == -1] = 0
