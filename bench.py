@@ -481,7 +481,7 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
 
     easy = rx_line(30.0)
     # threshold search (untimed): mean decoder iterations per candidate SNR, averaged over ranks
-    cands = [29.0, 28.0, 27.5, 27.0, 26.5, 26.0, 25.5, 25.0, 24.5, 24.0]
+    cands = [29.0, 28.0, 27.5, 27.0, 26.5, 26.25, 26.0, 25.5, 25.0, 24.0]
     its = []
     for snr in cands:
         channel(snr)
