@@ -799,6 +799,22 @@ def main():
                 "gather_ms": round(tm["gather_s"] * 1e3, 3),
                 "decode_ms": round(tm["decode_s"] * 1e3, 3),
                 "gather_bytes": tm["gather_bytes"], "ranks": world}
+        # algo='BF' / 'BP' (nr_decode_ldpc's other two algorithms) on 1024 codeblocks of the
+        # headline shape, float64 LLRs, L iterations (all run at -3 dB)
+        Bb = min(B, 1024)
+        x64 = llr[:Bb].double()
+        for algo in ("BF", "BP"):
+            nb = max(3, args.steps // 4)
+            wb, eb = timed(torch, dist, world,
+                           lambda: D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0), nb, 1)
+            _, stb, itb = D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0)
+            ex[f"{algo.lower()}_decode"] = {
+                "codeblocks_per_call": Bb, "codeblocks_per_s": round(Bb * world * nb / wb, 1),
+                "launch_ms": round(eb / nb * 1e3, 4), "mean_iterations": round(itb.float().mean().item(), 3),
+                "note": ("hard-decision bit flipping (ldpc_decoder_bit_flipping.py:5-73)" if algo == "BF" else
+                         "float64 sum-product flooding (_BP_process, nr_ldpc_decode.py:145-176), per-edge "
+                         "messages in a device scratch")}
+        del x64
         ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2))
         ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
         res["extras"] = ex

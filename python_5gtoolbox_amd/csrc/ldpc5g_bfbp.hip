@@ -12,7 +12,8 @@
 //        [B][E][Zc] (coalesced over z); APP and the row-ascending accumulator are in LDS as in
 //        the min-sum flooding kernel.
 // Thread mapping as the min-sum decoder: one thread per check row z, G = 384/Zc codeblocks
-// per workgroup.
+// per workgroup.  BP walks the rows with a runtime loop (scalar table reads, tanh / atanh inlined
+// once) and parks tanh(Lq/2) in the message scratch between its two passes: no per-thread arrays.
 #include <stdint.h>
 
 #include "ldpc5g_common.h"
@@ -46,11 +47,6 @@ template <int BG>
 constexpr ColLists<BG> kCols{};
 
 constexpr int kBfThreads = 384;
-
-// Out-of-line float64 transcendentals: BP calls them at every one of the 316 unrolled edges,
-// and inlining the math library there multiplies code size (and compile time) ~20x.
-__device__ __noinline__ double bp_tanh_half(double q) { return tanh(q / 2); }
-__device__ __noinline__ double bp_two_atanh(double x) { return 2.0 * atanh(x); }
 
 // ------------------------------------------------------------------------------------- BF
 template <int BG, typename T>
@@ -107,28 +103,29 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bf_kernel(
             if (z == 0) status[cb] = 1, iters[cb] = it;
             active = false;
         }
-        // ---- En = (2S - 1) H per column; flip all bits at the maximum (:61-70)
-        int en[NB];
-        int m = -(1 << 30);
-        sfor<0, NB>([&](auto jc) {
+        // ---- En = (2S - 1) H per column; flip all bits at the maximum (:61-70).  The column sums
+        //      are formed twice (for the maximum, then for the flips) rather than kept in a
+        //      per-thread array of NB ints, which lived in scratch
+        auto en_of = [&](auto jc) -> int {
             constexpr int j = decltype(jc)::value;
             int acc = 0;
             sfor<kCols<BG>.start[j], kCols<BG>.start[j + 1]>([&](auto xc) {
                 constexpr int x = decltype(xc)::value;
                 constexpr int i = kCols<BG>.row[x], e = kCols<BG>.edge[x];
                 // row i*Zc+m connects column j*Zc+(m+V)%Zc, so column z meets row m=(z-V)%Zc
-                if (active) acc += 2 * S[i * kCS + rotm(shift_of<BG>(zi, e))] - 1;
+                acc += 2 * S[i * kCS + rotm(shift_of<BG>(zi, e))] - 1;
             });
-            en[j] = acc;
-            m = acc > m ? acc : m;
-        });
+            return acc;
+        };
+        int m = -(1 << 30);
+        if (active) sfor<0, NB>([&](auto jc) { const int v = en_of(jc); m = v > m ? v : m; });
         if (active) atomicMax(&mx[cl], m);
         __syncthreads();
         if (active) {
             const int M = mx[cl];
             sfor<0, NB>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                if (en[j] == M) hd[j * kCS + tz] ^= 1;
+                if (en_of(jc) == M) hd[j * kCS + tz] ^= 1;
             });
         }
         __syncthreads();
@@ -180,64 +177,66 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bp_kernel(
     for (; it < L; ++it) {
         bool fail = false;
         uint64_t hdx = 0;
-        sfor<0, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i], d = P::RS[i + 1] - P::RS[i];
+        // rows in ascending order (a runtime loop over the base graph's device tables: the row and
+        // edge indices are uniform, so their table reads are scalar loads, and tanh / atanh appear
+        // once in the code instead of at each of the 316 edges of an unrolled graph)
+        for (int i = 0; i < MB; ++i) {
+            const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0;
             if (active) {
-                double tq[d];
+                // pass 1: Lq = LQ - Lr (:129-131), tanh(Lq/2) (:152, :165) parked in the message
+                // slot (the thread's own), the zero count, and the products the three cases need
                 int nz = 0, zk = 0;
                 bool par = false;
-                sfor<0, d>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int j = P::COL[e0 + k];
-                    const double rold = mrow[(e0 + k) * Zc + z];
+                double prod = 1.0, pb = 1.0, pa = 1.0;   // all; before / after the first zero
+                for (int k = 0; k < d; ++k) {
+                    const int e = e0 + k, j = col_d<BG>(e);
+                    double* m = mrow + (int64_t)e * Zc + z;
+                    const double rold = *m;
                     double a;
-                    if constexpr (j < KC) a = app[j * kCS + rot(shift_of<BG>(zi, e0 + k))];
-                    else {
+                    if (j < KC) {
+                        a = app[j * kCS + rot(shift_of<BG>(zi, e))];
+                    } else {
                         a = llrx(i) + rold;   // LQ of the degree-1 column
                         hdx |= (uint64_t)(a < 0.0) << (i - 4);
                     }
                     par ^= a < 0.0;
-                    const double q = a - rold;   // Lq = LQ - Lr (:129-131)
-                    if (q == 0.0) ++nz, zk = k;
-                    tq[k] = bp_tanh_half(q);     // tanh(Lq/2) (:152, :165)
-                });
+                    const double q = a - rold;
+                    const double tq = tanh(q / 2);
+                    *m = tq;
+                    prod = k == 0 ? tq : prod * tq;   // np.prod: left to right
+                    if (q == 0.0) {
+                        if (nz == 0) zk = k;
+                        ++nz;
+                    } else if (nz == 0) {
+                        pb = k == 0 ? tq : pb * tq;
+                    } else {
+                        pa = k == zk + 1 ? tq : pa * tq;
+                    }
+                }
                 fail |= par;
-                // (:150-175) three cases on the number of zero Lq in the row
-                double prod = tq[0];
-#pragma unroll
-                for (int k = 1; k < d; ++k) prod *= tq[k];
-                double pz = 1.0, pz2 = 1.0;   // one zero: prod(t[0:zk]) * prod(t[zk+1:])
-#pragma unroll
+                // pass 2 (:150-175): three cases on the number of zero Lq in the row
+                const double pzero = pb * pa;   // prod(t[0:zk]) * prod(t[zk+1:])
                 for (int k = 0; k < d; ++k) {
-                    if (k < zk) pz = (k == 0) ? tq[0] : pz * tq[k];
-                }
-#pragma unroll
-                for (int k = 0; k < d; ++k) {
-                    if (k > zk) pz2 = (k == zk + 1) ? tq[k] : pz2 * tq[k];
-                }
-                const double pzero = pz * pz2;
-                sfor<0, d>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int j = P::COL[e0 + k];
+                    const int e = e0 + k, j = col_d<BG>(e);
+                    double* m = mrow + (int64_t)e * Zc + z;
                     double r;
                     if (nz == 0) {
-                        const double tmp2 = prod / tq[k];
-                        r = tmp2 >= 1.0 ? kClip : (tmp2 <= -1.0 ? -kClip : bp_two_atanh(tmp2));
+                        const double tmp2 = prod / *m;
+                        r = tmp2 >= 1.0 ? kClip : (tmp2 <= -1.0 ? -kClip : 2.0 * atanh(tmp2));
                     } else if (nz == 1) {
                         r = (k == zk) ? pzero : 0.0;
                     } else {
                         r = 0.0;
                     }
-                    mrow[(e0 + k) * Zc + z] = r;
-                    if constexpr (j < KC) {
-                        double& a = acc[j * kCS + rot(shift_of<BG>(zi, e0 + k))];
-                        a = a + r;   // row-ascending accumulation (:126)
+                    *m = r;
+                    if (j < KC) {
+                        double& ac = acc[j * kCS + rot(shift_of<BG>(zi, e))];
+                        ac = ac + r;   // row-ascending accumulation (:126)
                     }
-                });
+                }
             }
             __syncthreads();
-        });
+        }
         if (active && fail) flag[cl] = 1;
         __syncthreads();
         if (active && flag[cl] == 0) {   // syndrome of LQ at pass start was 0 (:107-114)
@@ -259,29 +258,26 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bp_kernel(
     // ---- exhausted: ck = LQ <= 0, status = syndrome == 0 (:133-143)
     if (active) {
         bool fail = false;
-        sfor<0, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
+        for (int i = 0; i < MB; ++i) {
+            const int e0 = row_start_d<BG>(i), e1 = row_start_d<BG>(i + 1);
             bool par = false;
-            sfor<P::RS[i], P::RS[i + 1]>([&](auto ec) {
-                constexpr int e = decltype(ec)::value;
-                constexpr int j = P::COL[e];
-                double a;
-                if constexpr (j < KC) a = app[j * kCS + rot(shift_of<BG>(zi, e))];
-                else a = llrx(i) + mrow[e * Zc + z];
+            for (int e = e0; e < e1; ++e) {
+                const int j = col_d<BG>(e);
+                const double a = j < KC ? app[j * kCS + rot(shift_of<BG>(zi, e))]
+                                        : llrx(i) + mrow[(int64_t)e * Zc + z];
                 par ^= a <= 0.0;
-            });
+            }
             fail |= par;
-        });
+        }
         if (fail) flag[cl] = 1;
     }
     __syncthreads();
     if (active) {
         for (int j = 0; j < KC; ++j) crow[j * Zc + z] = (int8_t)(app[j * kCS + tz] <= 0.0);
-        sfor<4, MB>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int el = P::RS[i + 1] - 1;   // the ext column is the row's last edge
-            crow[(KB + i) * Zc + z] = (int8_t)(llrx(i) + mrow[el * Zc + z] <= 0.0);
-        });
+        for (int i = 4; i < MB; ++i) {
+            const int el = row_start_d<BG>(i + 1) - 1;   // the ext column is the row's last edge
+            crow[(KB + i) * Zc + z] = (int8_t)(llrx(i) + mrow[(int64_t)el * Zc + z] <= 0.0);
+        }
         if (z == 0) status[cb] = flag[cl] == 0, iters[cb] = L;
     }
 }
