@@ -42,6 +42,12 @@ constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 constexpr int kAPre = LDPC5G_FLOOD_APRE;
 // phase B: edge k's sign bit by one shift of the row's sign word (u << k) per edge it adds, instead
 // of shifting the word once per edge of the row (the LDS rows' halves add alternate edges)
+// phase A: a part's rows processed two at a time with their edges interleaved (two independent
+// dependency chains per wave between the per-edge volatile asm points), non-DEAD kernels only
+#ifndef LDPC5G_FLOOD_PAIR
+#define LDPC5G_FLOOD_PAIR 0
+#endif
+constexpr bool kPair = LDPC5G_FLOOD_PAIR != 0;
 #ifndef LDPC5G_FLOOD_BSHIFT
 #define LDPC5G_FLOOD_BSHIFT 0
 #endif
@@ -64,6 +70,8 @@ struct FloodPlan {
     int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner part's ext rows
     int xlist[NP][64] = {};   // ext rows of each part, ascending
     int nx[NP] = {};
+    int rlist[NP][64] = {};   // rows of each part (phase A owner), ascending
+    int nr[NP] = {};
     static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
     constexpr FloodPlan() {
         using P = BGT<BG>;
@@ -122,6 +130,7 @@ struct FloodPlan {
             xpos[i] = nx[owner[i]];
             xlist[owner[i]][nx[owner[i]]++] = i;
         }
+        for (int i = 0; i < P::MB; ++i) rlist[owner[i]][nr[owner[i]]++] = i;
         for (int j = 0; j < P::KC; ++j) {
             first_row[j] = -1;
             for (int i = 0; i < P::MB && first_row[j] < 0; ++i)
@@ -423,68 +432,94 @@ __device__ __forceinline__ void flood_body(
                 xr[p % XP] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][p]);
         };
         // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202)
-        auto rowA = [&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            constexpr int e0 = P::RS[i];
-            constexpr int d = P::RS[i + 1] - e0;
-            T mA, mB;
-            uint32_t u, idxo;   // u: bit 31 = sign of r_k for the edge k being visited
-            get_state(ic, mA, mB, u, idxo);
-            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-            uint32_t sx = 0, idx = 0, negs = 0;
-            bool par = false;
-            // core-edge LQ reads issued kAPre edges ahead of their use (ring ab)
-            constexpr int AP = kAPre > 0 ? kAPre : 1;
+        // core-edge LQ reads issued kAPre edges ahead of their use (ring ab)
+        constexpr int AP = kAPre > 0 ? kAPre : 1;
+        struct RowSt {
+            T mA, mB, min1, min2;
+            uint32_t u, idxo, sx, idx, negs;   // u: bit 31 = sign of r_k for the edge k being visited
+            bool par;
             T ab[AP];
-            auto aload = [&](auto kc2) {
-                constexpr int k2 = decltype(kc2)::value;
-                if constexpr (kAPre > 0 && k2 < d) {
-                    if constexpr (P::COL[e0 + k2] < KC) ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + rot(sh(e0 + k2)));
-                }
-            };
-            sfor<0, AP>([&](auto kc2) { aload(kc2); });
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int j = P::COL[e0 + k];
-                const T rold = xsign_v(pick(idxo == (uint32_t)k, mB, mA), u, mv);
-                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1, all-VGPR form
-                T a;
-                if constexpr (j < KC) {
-                    if constexpr (kAPre > 0) {
-                        a = ab[k % AP];
-                        aload(std::integral_constant<int, k + AP>{});
-                        if constexpr (kASb) __builtin_amdgcn_sched_barrier(0);
-                    } else {
-                        a = at(j * CS * TS + rot(sh(e0 + k)));
-                    }
+        };
+        auto aload = [&](RowSt& r, auto ic, auto kc2) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = P::RS[i + 1] - e0;
+            constexpr int k2 = decltype(kc2)::value;
+            if constexpr (kAPre > 0 && k2 < d) {
+                if constexpr (P::COL[e0 + k2] < KC) r.ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + rot(sh(e0 + k2)));
+            }
+        };
+        auto rbegin = [&](RowSt& r, auto ic) {
+            get_state(ic, r.mA, r.mB, r.u, r.idxo);
+            r.min1 = FT<T>::inf(), r.min2 = FT<T>::inf();
+            r.sx = 0, r.idx = 0, r.negs = 0;
+            r.par = false;
+            sfor<0, AP>([&](auto kc2) { aload(r, ic, kc2); });
+        };
+        auto rstep = [&](RowSt& r, auto ic, auto kc) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i];
+            constexpr int k = decltype(kc)::value;
+            constexpr int j = P::COL[e0 + k];
+            const T rold = xsign_v(pick(r.idxo == (uint32_t)k, r.mB, r.mA), r.u, mv);
+            asm("v_add_u32 %0, %1, %1" : "=v"(r.u) : "v"(r.u));   // u <<= 1, all-VGPR form
+            T a;
+            if constexpr (j < KC) {
+                if constexpr (kAPre > 0) {
+                    a = r.ab[k % AP];
+                    aload(r, ic, std::integral_constant<int, k + AP>{});
+                    if constexpr (kASb) __builtin_amdgcn_sched_barrier(0);
                 } else {
-                    constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
-                    if constexpr (kXPre > 0) {
-                        a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
-                        xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
-                    } else {
-                        a = llrx(i) + rold;
-                    }
-                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                    a = at(j * CS * TS + rot(sh(e0 + k)));
                 }
-                par ^= a < T(0);
-                const T q = a - rold;
-                const T aq = fabs(q);
-                idx = aq < min1 ? (uint32_t)k : idx;
-                asm volatile("" : "+v"(idx));   // update in place: a sunk select chain keeps all
-                                                // the compare masks live (scratch spills)
-                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
-                two_min(min1, min2, aq);
-                sx ^= FT<T>::sbits(q);
-            });
-            fail |= par;
-            T x1 = min1, x2 = min2;
+            } else {
+                constexpr int hh = kFloodPlan<BG, T, NP, CS>.owner[i], p = kFloodPlan<BG, T, NP, CS>.xpos[i];
+                if constexpr (kXPre > 0) {
+                    a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
+                    xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+                } else {
+                    a = llrx(i) + rold;
+                }
+                hdx |= (uint64_t)(a < T(0)) << (i - 4);
+            }
+            r.par ^= a < T(0);
+            const T q = a - rold;
+            const T aq = fabs(q);
+            r.idx = aq < r.min1 ? (uint32_t)k : r.idx;
+            asm volatile("" : "+v"(r.idx));   // update in place: a sunk select chain keeps all
+                                              // the compare masks live (scratch spills)
+            r.negs = __builtin_amdgcn_alignbit(r.negs, FT<T>::sbits(q), 31);
+            two_min(r.min1, r.min2, aq);
+            r.sx ^= FT<T>::sbits(q);
+        };
+        auto rend = [&](RowSt& r, auto ic) {
+            constexpr int i = decltype(ic)::value, d = P::RS[i + 1] - P::RS[i];
+            fail |= r.par;
+            T x1 = r.min1, x2 = r.min2;
             if constexpr (OFS) {
-                x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
+                x1 = r.min1 - beta, x2 = r.min2 - beta;   // max(minv - beta, 0) (:201)
                 x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
             }
-            const uint32_t flip = (uint32_t)((int32_t)sx >> 31) & ((1u << d) - 1u);
-            put_state(ic, alpha * x1, alpha * x2, negs ^ flip, idx);
+            const uint32_t flip = (uint32_t)((int32_t)r.sx >> 31) & ((1u << d) - 1u);
+            put_state(ic, alpha * x1, alpha * x2, r.negs ^ flip, r.idx);
+        };
+        auto rowA = [&](auto ic) {
+            constexpr int i = decltype(ic)::value, d = P::RS[i + 1] - P::RS[i];
+            RowSt r;
+            rbegin(r, ic);
+            sfor<0, d>([&](auto kc) { rstep(r, ic, kc); });
+            rend(r, ic);
+        };
+        // two rows with their edges interleaved (edge k of A, then edge k of B)
+        auto rowA2 = [&](auto ica, auto icb) {
+            constexpr int da = P::RS[decltype(ica)::value + 1] - P::RS[decltype(ica)::value];
+            constexpr int db = P::RS[decltype(icb)::value + 1] - P::RS[decltype(icb)::value];
+            RowSt ra, rb;
+            rbegin(ra, ica);
+            rbegin(rb, icb);
+            sfor<0, (da > db ? da : db)>([&](auto kc) {
+                if constexpr (decltype(kc)::value < da) rstep(ra, ica, kc);
+                if constexpr (decltype(kc)::value < db) rstep(rb, icb, kc);
+            });
+            rend(ra, ica);
+            rend(rb, icb);
         };
         // dead extension row: LQ_ext = 0 + r_old_ext (its syndrome bit), q_core = LQ - (+-0);
         // new state as the full update leaves it up to zero signs: nA = 0, nB = alpha * max(
@@ -526,17 +561,35 @@ __device__ __forceinline__ void flood_body(
         };
         if (active) {
             per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
-            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
-                constexpr int i = decltype(ic)::value;
-                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
-                    if constexpr (DEAD && i >= 4) {
-                        if (rdead(ic)) rowA_dead(ic);
-                        else rowA(ic);
-                    } else {
-                        rowA(ic);
+            if constexpr (kPair && !DEAD) {
+                // each part's rows in pairs, one pair per scheduling region
+                per_half([&](auto hc) {
+                    constexpr int hh = decltype(hc)::value, nr = kFloodPlan<BG, T, NP, CS>.nr[hh];
+                    sfor<0, (nr + 1) / 2>([&](auto pc2) {
+                        constexpr int x = 2 * decltype(pc2)::value;
+                        constexpr int ia = kFloodPlan<BG, T, NP, CS>.rlist[hh][x];
+                        if constexpr (x + 1 < nr) {
+                            constexpr int ib = kFloodPlan<BG, T, NP, CS>.rlist[hh][x + 1];
+                            rowA2(std::integral_constant<int, ia>{}, std::integral_constant<int, ib>{});
+                        } else {
+                            rowA(std::integral_constant<int, ia>{});
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                });
+            } else {
+                sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
+                    constexpr int i = decltype(ic)::value;
+                    if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
+                        if constexpr (DEAD && i >= 4) {
+                            if (rdead(ic)) rowA_dead(ic);
+                            else rowA(ic);
+                        } else {
+                            rowA(ic);
+                        }
                     }
-                }
-            });
+                });
+            }
             if (fail) flagA[cl] = 1;
         }
         // phase B's shift words are loaded one row group ahead (scalar loads issued before the
