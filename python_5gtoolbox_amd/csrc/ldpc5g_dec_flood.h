@@ -53,6 +53,29 @@ constexpr bool kPair = LDPC5G_FLOOD_PAIR != 0;
 #endif
 constexpr bool kBShift = LDPC5G_FLOOD_BSHIFT != 0;
 constexpr bool kASb = LDPC5G_FLOOD_ASB != 0;
+// phase A takes its rotated core-edge offsets from an LDS wrap table (one LDS read issued two edges
+// ahead instead of the add/add/min arithmetic: 3 half-rate VALU ops per edge) in the float64 BG1
+// batch kernel, whose LDS has room for it (2 x 384 u32 entries; the state rows still number 10).
+// r04: 4.04 -> 3.93 ms per 4096 codeblocks.  (Phase B keeps the arithmetic: a table read there
+// adds an LDS round trip to each barrier-separated row group, measured 4.08 ms.)
+template <int BG, typename T, int NP, int CS>
+constexpr bool flood_wtab() { return BG == 1 && sizeof(T) == 8 && NP == 2 && CS == 384; }
+template <int BG, typename T, int NP, int CS>
+constexpr int flood_wtab_bytes() { return flood_wtab<BG, T, NP, CS>() ? 2 * CS * 4 : 0; }
+// ZC > 0: a kernel for that one lifting size (Zc = 384 = CS, one codeblock per workgroup): the
+// shifts V(i,j) mod Zc are compile-time constants, so the wrap-table reads take them as immediate
+// offsets and no shift word is loaded or unpacked (r04: 3.93 -> 3.64 ms per 4096 codeblocks)
+template <int ZC>
+constexpr int zc_set() {
+    for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
+        if (kLdpcZcList[i] == ZC) return kLdpcZcSet[i];
+    return 0;
+}
+template <int BG, int ZC>
+constexpr int zc_shift(int e) {
+    if constexpr (BG == 1) return kBG1Shift[zc_set<ZC>()][e] % ZC;
+    else return kBG2Shift[zc_set<ZC>()][e] % ZC;
+}
 
 // Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
 // state lives, and the packing of its sign word.  NP = 2, CS = 384 for batches; NP = 16, CS = 64 for
@@ -76,7 +99,7 @@ struct FloodPlan {
     constexpr FloodPlan() {
         using P = BGT<BG>;
         const auto& G = kGroups<BG>;
-        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4;
+        const size_t fixed = (size_t)P::KC * CS * sizeof(T) + (2 * kMaxG + 4) * 4 + flood_wtab_bytes<BG, T, NP, CS>();
         const int fit = (int)((kLdsPerCU - fixed) / (CS * (2 * sizeof(T) + 4)));
         int lead = 0;   // leading single-row groups: their phase B is split only if in LDS
         while (lead < G.n && G.start[lead + 1] - G.start[lead] == 1 && G.start[lead] == lead) ++lead;
@@ -160,7 +183,7 @@ static_assert(first_rows_core<1>() && first_rows_core<2>(), "dead-row skipping n
 template <int BG, typename T, int NP, int CS>
 constexpr size_t flood_lds_bytes_t() {
     return (size_t)BGT<BG>::KC * CS * sizeof(T) + (size_t)kFloodPlan<BG, T, NP, CS>.nls * CS * (2 * sizeof(T) + 4) +
-           (2 * kMaxG + 4) * 4;
+           (2 * kMaxG + 4) * 4 + flood_wtab_bytes<BG, T, NP, CS>();
 }
 
 // x with its sign flipped by bit 31 of u (all-VGPR v_bitop3: x ^ (u & mv), mv = 0x80000000)
@@ -190,7 +213,7 @@ __device__ __forceinline__ void two_min(double& m1, double& m2, double a) {
     m1 = fmin(m1, a);
 }
 
-template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD>
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD, int ZCC = 0>
 __device__ __forceinline__ void flood_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -218,6 +241,10 @@ __device__ __forceinline__ void flood_body(
         DecWork w = work[blockIdx.x];
         Zc = w.Zc, zi = w.zi, G = w.G;
     }
+    constexpr bool kZ = ZCC > 0;   // compile-time lifting size (see zc_shift)
+    static_assert(!kZ || (ZCC == CS && flood_wtab<BG, T, NP, CS>()), "Zc-specialised kernel: Zc = CS, wrap table");
+    constexpr bool WT = flood_wtab<BG, T, NP, CS>();
+    if constexpr (kZ) Zc = ZCC, G = 1;
     // slot s = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
     // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
     const int z = s / G;
@@ -247,6 +274,7 @@ __device__ __forceinline__ void flood_body(
     const int tzb = so * TS;   // byte offset of this slot's own column entry
     const int zg = valid ? z : 0;   // loads issued without a branch stay in row 0 of CB 0
     int zv = zg, ziv = zi;
+    constexpr int TBL_B = FLAG_B + (2 * kMaxG + 4) * 4;   // wrap table (WT)
     int* flagA = (int*)(smem + FLAG_B);
     int* anyf = flagA + 2 * kMaxG;
     int epoch = 0;
@@ -347,6 +375,13 @@ __device__ __forceinline__ void flood_body(
     }
     if (s == 0 && h == 0)
         for (int c = 0; c < G; ++c) flagA[c] = 0;
+    if constexpr (WT) {   // entry e (e < 2*Zc*G): byte offset of column entry e mod (Zc*G)
+        const int ZG = Zc * G;
+        if (t < ZG) {
+            *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(uint32_t)(TBL_B + t * 4) = (uint32_t)(t * TS);
+            *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(uint32_t)(TBL_B + (t + ZG) * 4) = (uint32_t)(t * TS);
+        }
+    }
     uint32_t* livew = (uint32_t*)(anyf + 2);   // workgroup OR of nzx (2 words)
     if (t == 0) *anyf = 0;
     if constexpr (DEAD)
@@ -383,9 +418,13 @@ __device__ __forceinline__ void flood_body(
     // kernel's LDS wrap table: phase B is a chain of dependent LDS round trips per row group, and
     // a table lookup adds one (measured: 4.85 -> 4.53 ms per 4096 f64 codeblocks without it)
     const uint32_t GT = (uint32_t)(G * TS), tzbw = (uint32_t)tzb - (uint32_t)(Zc * G * TS);
+    const uint32_t G4 = (uint32_t)(G * 4), tzT = (uint32_t)(TBL_B + so * 4);
+    uint32_t tzbR = (uint32_t)tzb, tzbwR = tzbw;   // kZ: made opaque per iteration (no LICM)
+    uint32_t tzTR = tzT;   // opaque: the table's base stays in the VGPR, shift offsets are immediates
     auto rot = [&](int sft) -> int {
         const uint32_t S = (uint32_t)sft * GT;
-        return (int)min((uint32_t)tzb + S, tzbw + S);
+        if constexpr (kZ) return (int)min(tzbR + S, tzbwR + S);
+        else return (int)min((uint32_t)tzb + S, tzbw + S);
     };
     // the same on the VALU (v_mul_u32_u24 with an opaque VGPR stride) for the final syndrome pass:
     // the scalar unit is shared by the workgroup's 12 waves
@@ -414,11 +453,21 @@ __device__ __forceinline__ void flood_body(
         ziv = zi;
         asm volatile("" : "+v"(zv));
         asm volatile("" : "+s"(ziv));
+        if constexpr (kZ) {
+            tzbR = (uint32_t)tzb, tzbwR = tzbw;
+            asm volatile("" : "+v"(tzbR));
+            asm volatile("" : "+v"(tzbwR));
+        }
+        if constexpr (WT) {
+            tzTR = tzT;
+            asm volatile("" : "+v"(tzTR));
+        }
         bool fail = false;
         uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
         // shift words of this lifting size: one base pointer (SGPR pair), immediate offsets
         const uint32_t* __restrict__ swrow = shift_row<BG>(ziv);
         auto sh = [&](int e) -> int {   // e compile-time after unrolling
+            if constexpr (kZ) return zc_shift<BG, ZCC>(e);
             const uint32_t w = swrow[e >> 1];
             return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
         };
@@ -439,12 +488,24 @@ __device__ __forceinline__ void flood_body(
             uint32_t u, idxo, sx, idx, negs;   // u: bit 31 = sign of r_k for the edge k being visited
             bool par;
             T ab[AP];
+            uint32_t tb[AP + 1];   // WT: wrap-table entries of the next AP + 1 edges
+        };
+        auto aloadt = [&](RowSt& r, auto ic, auto kc3) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = P::RS[i + 1] - e0;
+            constexpr int k3 = decltype(kc3)::value;
+            if constexpr (WT && k3 < d) {
+                if constexpr (P::COL[e0 + k3] < KC)
+                    r.tb[k3 % (AP + 1)] = *(lds_u32*)(uintptr_t)(tzTR + (uint32_t)sh(e0 + k3) * G4);
+            }
         };
         auto aload = [&](RowSt& r, auto ic, auto kc2) {
             constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = P::RS[i + 1] - e0;
             constexpr int k2 = decltype(kc2)::value;
             if constexpr (kAPre > 0 && k2 < d) {
-                if constexpr (P::COL[e0 + k2] < KC) r.ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + rot(sh(e0 + k2)));
+                if constexpr (P::COL[e0 + k2] < KC) {
+                    if constexpr (WT) r.ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + (int)r.tb[k2 % (AP + 1)]);
+                    else r.ab[k2 % AP] = at(P::COL[e0 + k2] * CS * TS + rot(sh(e0 + k2)));
+                }
             }
         };
         auto rbegin = [&](RowSt& r, auto ic) {
@@ -452,6 +513,7 @@ __device__ __forceinline__ void flood_body(
             r.min1 = FT<T>::inf(), r.min2 = FT<T>::inf();
             r.sx = 0, r.idx = 0, r.negs = 0;
             r.par = false;
+            if constexpr (WT) sfor<0, AP + 1>([&](auto kc3) { aloadt(r, ic, kc3); });
             sfor<0, AP>([&](auto kc2) { aload(r, ic, kc2); });
         };
         auto rstep = [&](RowSt& r, auto ic, auto kc) {
@@ -465,6 +527,7 @@ __device__ __forceinline__ void flood_body(
                 if constexpr (kAPre > 0) {
                     a = r.ab[k % AP];
                     aload(r, ic, std::integral_constant<int, k + AP>{});
+                    aloadt(r, ic, std::integral_constant<int, k + AP + 1>{});
                     if constexpr (kASb) __builtin_amdgcn_sched_barrier(0);
                 } else {
                     a = at(j * CS * TS + rot(sh(e0 + k)));
@@ -676,6 +739,7 @@ __device__ __forceinline__ void flood_body(
                 prefetch_state(std::integral_constant<int, g + 1>{});
             }
             auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                if constexpr (kZ) return zc_shift<BG, ZCC>(e);
                 const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
                 return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
             };
@@ -812,14 +876,14 @@ __device__ __forceinline__ void flood_body(
 
 // NP parts x CS slots: 768 threads (3 waves per SIMD) for batches, 1024 (4 per SIMD) for the
 // 16-part configuration of small launches
-template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false, int ZCC = 0>
 __global__ __launch_bounds__(NP * CS) __attribute__((amdgpu_waves_per_eu(NP * CS / 256))) void
 ldpc_flood_kernel(LDPC5G_DEC_PARAMS) {
-    flood_body<BG, T, OFS, NP, CS, DEAD>(LDPC5G_DEC_ARGS);
+    flood_body<BG, T, OFS, NP, CS, DEAD, ZCC>(LDPC5G_DEC_ARGS);
 }
 
-template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false>
-constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS, DEAD>; }
+template <int BG, typename T, bool OFS, int NP, int CS, bool DEAD = false, int ZCC = 0>
+constexpr auto flood_kernel() { return ldpc_flood_kernel<BG, T, OFS, NP, CS, DEAD, ZCC>; }
 
 template <int BG, typename T, int NP, int CS>
 size_t flood_lds_bytes() {
@@ -827,23 +891,24 @@ size_t flood_lds_bytes() {
     return flood_lds_bytes_t<BG, T, NP, CS>();
 }
 
-template <int BG, typename T, int NP, int CS, bool DEAD = false>
+template <int BG, typename T, int NP, int CS, bool DEAD = false, int ZCC = 0>
 int set_flood_lds(bool ofs) {
     const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
-    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS, DEAD>()>(lds)
-               : set_lds_once<flood_kernel<BG, T, false, NP, CS, DEAD>()>(lds);
+    return ofs ? set_lds_once<flood_kernel<BG, T, true, NP, CS, DEAD, ZCC>()>(lds)
+               : set_lds_once<flood_kernel<BG, T, false, NP, CS, DEAD, ZCC>()>(lds);
 }
 
 // G codeblocks per workgroup (G * Zc <= CS); NP parts of H = G*Zc rounded up to a wave
-template <int BG, typename T, int NP, int CS, bool DEAD = false>
+template <int BG, typename T, int NP, int CS, bool DEAD = false, int ZCC = 0>
 int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
                      int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
                      hipStream_t st) {
     const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS, DEAD> : ldpc_flood_kernel<BG, T, false, NP, CS, DEAD>;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, NP, CS, DEAD, ZCC> : ldpc_flood_kernel<BG, T, false, NP, CS, DEAD, ZCC>;
     const int H = ((G * Zc + 63) / 64) * 64;
     if (G < 1 || H > CS) return fail(LDPC5G_ESIZE, "flooding launch: %d codeblocks of Zc=%d per workgroup", G, Zc);
-    if (int rc = set_flood_lds<BG, T, NP, CS, DEAD>(ofs)) return rc;
+    if (ZCC > 0 && (Zc != ZCC || G != 1)) return fail(LDPC5G_ESIZE, "Zc=%d kernel launched for Zc=%d, G=%d", ZCC, Zc, G);
+    if (int rc = set_flood_lds<BG, T, NP, CS, DEAD, ZCC>(ofs)) return rc;
     const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
     hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(NP * H), lds, st, llr, ck, status, iters, B, Zc,
                        zi, G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
@@ -859,6 +924,10 @@ int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, in
                    int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks
     const int G = std::min(dec_G(Zc, false), B);
+    if constexpr (flood_wtab<BG, T, kFloodNP, kFloodCS>())
+        if (Zc == kFloodCS)   // the largest lifting size has its own kernel (zc_shift)
+            return launch_flood_cfg<BG, T, kFloodNP, kFloodCS, DEAD, kFloodCS>(
+                llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);
     return launch_flood_cfg<BG, T, kFloodNP, kFloodCS, DEAD>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
                                                              alpha, beta, pc, st);
 }

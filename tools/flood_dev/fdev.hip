@@ -27,7 +27,5 @@ extern "C" int fdev_decode(const double* llr, int8_t* ck, uint8_t* status, int32
     for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
         if (kLdpcZcList[i] == Zc) zi = i;
     if (zi < 0) return LDPC5G_EZC;
-    const int G = std::min(dec_G(Zc, false), B);
-    return launch_flood_cfg<1, double, kFloodNP, kFloodCS>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
-                                                           alpha, 0.0, 2, st);
+    return launch_flood_t<1, double>(llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, 0.0, 2, st);
 }
