@@ -38,9 +38,10 @@ HBM_PEAK_GBS = 8000.0                                # MI355X_MICROARCH.md chip 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 # exact kernel names as rocprofv3 reports them for the 4096-codeblock BG1 Zc=384 launches (the
 # flooding kernel's 4th/5th template arguments are its plan: 2 parts x 384 slots; the last one of
-# both kernels is DEAD, the LDPC5G_RATE_MATCHED variant, false for the headline)
-DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false, false>",
-              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false>"}
+# both kernels is DEAD, the LDPC5G_RATE_MATCHED variant, false for the headline; then the
+# compile-time lifting size, 384 for the Zc = 384 kernels, 0 for the runtime-Zc ones)
+DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false, false, 384>",
+              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false, 0>"}
 DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384, false, 384>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 

@@ -102,6 +102,21 @@ __device__ __forceinline__ uint32_t shift_word(int zi, int w) {
 }
 
 
+// Kernels for one lifting size (template argument ZCC > 0; used for Zc = 384, the size of every
+// large codeblock): the shifts V(i,j) mod Zc are compile-time constants, so wrap-table reads take
+// them as immediate offsets and no shift word is loaded from memory or unpacked on the scalar unit.
+template <int ZC>
+constexpr int zc_set() {
+    for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
+        if (kLdpcZcList[i] == ZC) return kLdpcZcSet[i];
+    return 0;
+}
+template <int BG, int ZC>
+constexpr int zc_shift(int e) {
+    if constexpr (BG == 1) return kBG1Shift[zc_set<ZC>()][e] % ZC;
+    else return kBG2Shift[zc_set<ZC>()][e] % ZC;
+}
+
 // Layered: the (mA, mB) magnitudes of the first kLdsRows rows live in LDS rather than VGPRs, so
 // the kernel fits the 168-VGPR budget of 3 waves/SIMD without scratch spills (spilling kernels
 // are held to fewer resident waves).  2 x (40 KB APP + 33 KB state + 3 KB flags) <= 160 KB.
@@ -309,7 +324,7 @@ __device__ __forceinline__ void ck_store_staged(int NFZ, int nslots, SlotDst&& s
 // its clamp at 0 are compiled out (min >= +0 already; the result is identical).
 // DEAD = true: the variant for rate-recovered inputs (LDPC5G_RATE_MATCHED), which detects and
 // skips dead extension rows; DEAD = false compiles none of that (the headline kernel).
-template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false>
+template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false, int ZCC = 0>
 __device__ __forceinline__ void dec_body(
     const T* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int B, int Zc_u, int zi_u, int G_u, int64_t ldl, int64_t ldc,
@@ -337,6 +352,9 @@ __device__ __forceinline__ void dec_body(
         DecWork w = work[blockIdx.x];
         Zc = w.Zc, zi = w.zi, G = w.G;
     }
+    constexpr bool kZ = ZCC > 0;   // compile-time lifting size (zc_shift): G = CS / ZCC slots
+    static_assert(!kZ || CS % ZCC == 0, "Zc-specialised layered kernel");
+    if constexpr (kZ) Zc = ZCC, G = CS / ZCC;
     // thread t = z*G + cl owns row z of codeblock slot cl; LDS column entries are interleaved the
     // same way (entry (z, cl) at byte (z*G + cl)*TS), so a cyclic shift never crosses CB slots
     const int z = t / G;
@@ -487,7 +505,11 @@ __device__ __forceinline__ void dec_body(
             *(lds_u32*)(uintptr_t)(uint32_t)(TBL_B + (t + ZG) * 4) = (uint32_t)(t * 4);
         }
     }
-    const uint32_t tzbT = (uint32_t)(TBL_B + (valid ? t : 0) * 4);
+    const uint32_t tzbT0 = (uint32_t)(TBL_B + (valid ? t : 0) * 4);
+    // kZ: the table base and own offsets are re-made opaque each iteration, so the compile-time
+    // shift offsets stay immediates and LICM does not hoist ~300 constant addresses into VGPRs
+    uint32_t tzbT = tzbT0;
+    uint32_t tzbR = (uint32_t)tzb, tzbwR = tzbw;
     bool active = valid;
     lds_barrier();
     // Dead extension rows: a row whose degree-1 column has LLR +0.0 for every codeblock slot of the
@@ -522,7 +544,8 @@ __device__ __forceinline__ void dec_body(
     // one tzbw + s*GT is a valid (smaller) offset, otherwise it is negative, i.e. a huge unsigned.
     auto rot = [&](int s) -> int {
         const uint32_t S = (uint32_t)s * GT;
-        return (int)min((uint32_t)tzb + S, tzbw + S);
+        if constexpr (kZ) return (int)min(tzbR + S, tzbwR + S);
+        else return (int)min((uint32_t)tzb + S, tzbw + S);
     };
 
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
@@ -535,6 +558,12 @@ __device__ __forceinline__ void dec_body(
         ziv = zi;
         asm volatile("" : "+v"(zv));
         asm volatile("" : "+s"(ziv));
+        if constexpr (kZ) {
+            tzbT = tzbT0, tzbR = (uint32_t)tzb, tzbwR = tzbw;
+            asm volatile("" : "+v"(tzbT));
+            asm volatile("" : "+v"(tzbR));
+            asm volatile("" : "+v"(tzbwR));
+        }
         bool fail = false;
         uint64_t hdx = 0;   // ext hard decisions at the end of the pass
         // ---- layered row i: q = APP - r_old, APP = q + r_new.
@@ -655,6 +684,7 @@ __device__ __forceinline__ void dec_body(
         T xlb[2][NXR] = {};   // layered: ext-column LLRs of rows >= 4, double-buffered by group parity
         auto prefetch = [&](auto gc) {
             constexpr int g = decltype(gc)::value;
+            if constexpr (kZ) return;
             sfor<0, group_nw<BG>(g)>([&](auto wc) {
                 constexpr int w = decltype(wc)::value;
                 nsw[w] = shift_word<BG>(ziv, group_w0<BG>(g) + w);
@@ -682,6 +712,7 @@ __device__ __forceinline__ void dec_body(
                     prefetch_xl(std::integral_constant<int, g + 1>{});
             }
             auto gshift = [&](int e) -> int {   // e compile-time after unrolling
+                if constexpr (kZ) return zc_shift<BG, ZCC>(e);
                 const uint32_t w = csw[(e >> 1) - group_w0<BG>(g)];
                 return (int)((e & 1) ? (w >> 16) : (w & 0xffffu));
             };
@@ -725,7 +756,11 @@ __device__ __forceinline__ void dec_body(
                     const bool sf = syndrome_fails<BG, all_rows<BG>(), true, T, false>(
                         [&](auto ic, auto kc) -> T {
                             constexpr int e = P::RS[decltype(ic)::value] + decltype(kc)::value;
-                            return at(P::COL[e] * CS * TS + rot(shift_of<BG>(ziv, e)));
+                            if constexpr (kZ)   // the wrap table: immediate offsets, no VALU
+                                return at(P::COL[e] * CS * TS +
+                                          (int)*(lds_u32*)(uintptr_t)(tzbT + (uint32_t)zc_shift<BG, ZCC>(e) * GT));
+                            else
+                                return at(P::COL[e] * CS * TS + rot(shift_of<BG>(ziv, e)));
                         },
                         [&](auto ic) -> bool { return (hdx >> (decltype(ic)::value - 4)) & 1u; });
                     if (sf) flagB[clq] = 1;
@@ -841,15 +876,15 @@ __device__ __forceinline__ void dec_body(
     llr, ck, status, iters, B, Zc_u, zi_u, G_u, ldl, ldc, L, alpha, beta, pc, work, cbs
 
 // layered float32: 768 threads = 12 waves = 3 per SIMD (<= 168 VGPRs), G = floor(768/Zc) CBs
-template <int BG, typename T, bool LAYERED, bool OFS, bool DEAD = false>
+template <int BG, typename T, bool LAYERED, bool OFS, bool DEAD = false, int ZCC = 0>
 __global__ __launch_bounds__(kDecThreadsL) __attribute__((amdgpu_waves_per_eu(3))) void
 ldpc_dec_kernel_l(LDPC5G_DEC_PARAMS) {
-    dec_body<BG, T, LAYERED, OFS, DEAD>(LDPC5G_DEC_ARGS);
+    dec_body<BG, T, LAYERED, OFS, DEAD, ZCC>(LDPC5G_DEC_ARGS);
 }
-template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false>
+template <int BG, typename T, bool LAYERED, bool OFS = true, bool DEAD = false, int ZCC = 0>
 constexpr auto dec_kernel() {
     static_assert(LAYERED, "the flooding kernels are in ldpc5g_dec_flood.h");
-    return ldpc_dec_kernel_l<BG, T, LAYERED, OFS, DEAD>;
+    return ldpc_dec_kernel_l<BG, T, LAYERED, OFS, DEAD, ZCC>;
 }
 
 template <int BG, typename T, bool LAYERED>
@@ -858,23 +893,37 @@ size_t dec_lds_bytes() {
     return dec_lds_bytes_t<BG, T, LAYERED>();
 }
 
-template <int BG, typename T, bool LAYERED, bool DEAD = false>
-int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
-                 int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
-    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD>() : dec_kernel<BG, T, LAYERED, false, DEAD>();
-    // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
-    // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
-    const int G = std::min(dec_G(Zc, LAYERED), B);
+// the kernel for one (OFS, ZCC) pair
+template <int BG, typename T, bool LAYERED, bool DEAD, int ZCC>
+int launch_dec_zc(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                  int G, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD, ZCC>() : dec_kernel<BG, T, LAYERED, false, DEAD, ZCC>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
     const int threads = ((G * Zc + 63) / 64) * 64;
     const int grid = (B + G - 1) / G;
-    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD>()>(lds)
-                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD>()>(lds))
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD, ZCC>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD, ZCC>()>(lds))
         return rc;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, llr, ck, status, iters, B, Zc, zi,
                        G, ldl, ldc, L, (T)alpha, (T)beta, pc, (const DecWork*)nullptr,
                        (const CbRef*)nullptr);
     return check_hip(hipGetLastError(), "ldpc_dec_kernel launch");
+}
+
+template <int BG, typename T, bool LAYERED, bool DEAD = false>
+int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc, int zi,
+                 int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
+    // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
+    // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
+    const int G = std::min(dec_G(Zc, LAYERED), B);
+    constexpr int ZL = 384;   // BG1's largest lifting size has its own kernel (zc_shift; not
+                              // the DEAD variant, whose extra live registers then spill)
+    if constexpr (BG == 1 && !DEAD)
+        if (Zc == ZL && G == dec_cs<LAYERED>() / ZL)
+            return launch_dec_zc<BG, T, LAYERED, DEAD, ZL>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
+                                                           alpha, beta, pc, st);
+    return launch_dec_zc<BG, T, LAYERED, DEAD, 0>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha,
+                                                  beta, pc, st);
 }
 
 template <int BG, typename T, bool LAYERED, bool DEAD = false>

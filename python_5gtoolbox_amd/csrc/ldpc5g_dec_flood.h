@@ -62,20 +62,8 @@ template <int BG, typename T, int NP, int CS>
 constexpr bool flood_wtab() { return BG == 1 && sizeof(T) == 8 && NP == 2 && CS == 384; }
 template <int BG, typename T, int NP, int CS>
 constexpr int flood_wtab_bytes() { return flood_wtab<BG, T, NP, CS>() ? 2 * CS * 4 : 0; }
-// ZC > 0: a kernel for that one lifting size (Zc = 384 = CS, one codeblock per workgroup): the
-// shifts V(i,j) mod Zc are compile-time constants, so the wrap-table reads take them as immediate
-// offsets and no shift word is loaded or unpacked (r04: 3.93 -> 3.64 ms per 4096 codeblocks)
-template <int ZC>
-constexpr int zc_set() {
-    for (int i = 0; i < LDPC5G_NUM_ZC; ++i)
-        if (kLdpcZcList[i] == ZC) return kLdpcZcSet[i];
-    return 0;
-}
-template <int BG, int ZC>
-constexpr int zc_shift(int e) {
-    if constexpr (BG == 1) return kBG1Shift[zc_set<ZC>()][e] % ZC;
-    else return kBG2Shift[zc_set<ZC>()][e] % ZC;
-}
+// ZCC > 0 (zc_shift, ldpc5g_dec_body.h): a kernel for the one lifting size Zc = 384 = CS, one
+// codeblock per workgroup, r04: 3.93 -> 3.64 ms per 4096 codeblocks
 
 // Row plan of a workgroup of NP parts x CS slots (constexpr): which part runs each row, where its
 // state lives, and the packing of its sign word.  NP = 2, CS = 384 for batches; NP = 16, CS = 64 for

@@ -13,7 +13,7 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-KERNEL = "_ZN11ldpc5g_impl12_GLOBAL__N_117ldpc_dec_kernel_lILi1EfLb1ELb0EEEvPKT0_PaPhPiiiiilliS2_S2_iPKNS_7DecWorkEPKNS_5CbRefE"
+KERNEL = "_ZN11ldpc5g_impl12_GLOBAL__N_117ldpc_dec_kernel_lILi1EfLb1ELb0ELb0ELi384EEEvPKT0_PaPhPiiiiilliS2_S2_iPKNS_7DecWorkEPKNS_5CbRefE"
 
 
 def disasm(lib):
