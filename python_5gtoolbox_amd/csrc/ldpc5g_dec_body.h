@@ -506,10 +506,9 @@ __device__ __forceinline__ void dec_body(
         }
     }
     const uint32_t tzbT0 = (uint32_t)(TBL_B + (valid ? t : 0) * 4);
-    // kZ: the table base and own offsets are re-made opaque each iteration, so the compile-time
-    // shift offsets stay immediates and LICM does not hoist ~300 constant addresses into VGPRs
+    // kZ: the table base is re-made opaque each iteration, so the compile-time shift offsets stay
+    // immediates and LICM does not hoist ~300 constant addresses into VGPRs
     uint32_t tzbT = tzbT0;
-    uint32_t tzbR = (uint32_t)tzb, tzbwR = tzbw;
     bool active = valid;
     lds_barrier();
     // Dead extension rows: a row whose degree-1 column has LLR +0.0 for every codeblock slot of the
@@ -544,8 +543,7 @@ __device__ __forceinline__ void dec_body(
     // one tzbw + s*GT is a valid (smaller) offset, otherwise it is negative, i.e. a huge unsigned.
     auto rot = [&](int s) -> int {
         const uint32_t S = (uint32_t)s * GT;
-        if constexpr (kZ) return (int)min(tzbR + S, tzbwR + S);
-        else return (int)min((uint32_t)tzb + S, tzbw + S);
+        return (int)min((uint32_t)tzb + S, tzbw + S);
     };
 
     uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
@@ -559,10 +557,8 @@ __device__ __forceinline__ void dec_body(
         asm volatile("" : "+v"(zv));
         asm volatile("" : "+s"(ziv));
         if constexpr (kZ) {
-            tzbT = tzbT0, tzbR = (uint32_t)tzb, tzbwR = tzbw;
+            tzbT = tzbT0;
             asm volatile("" : "+v"(tzbT));
-            asm volatile("" : "+v"(tzbR));
-            asm volatile("" : "+v"(tzbwR));
         }
         bool fail = false;
         uint64_t hdx = 0;   // ext hard decisions at the end of the pass
@@ -916,9 +912,8 @@ int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int 
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
     // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
     const int G = std::min(dec_G(Zc, LAYERED), B);
-    constexpr int ZL = 384;   // BG1's largest lifting size has its own kernel (zc_shift; not
-                              // the DEAD variant, whose extra live registers then spill)
-    if constexpr (BG == 1 && !DEAD)
+    constexpr int ZL = 384;   // BG1's largest lifting size has its own kernel (zc_shift)
+    if constexpr (BG == 1)
         if (Zc == ZL && G == dec_cs<LAYERED>() / ZL)
             return launch_dec_zc<BG, T, LAYERED, DEAD, ZL>(llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L,
                                                            alpha, beta, pc, st);
