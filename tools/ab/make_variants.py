@@ -102,6 +102,17 @@ VARIANTS.update({
     "lay_combo": (LAYERED, [_NOINIT, _IDXOP] + _NOPF),
 })
 
+# r04, the Zc = 384 layered kernel (table reads with immediate offsets): how many rows keep their
+# rotated offsets live from pass 1 to pass 2, and how many rows keep their state in LDS
+VARIANTS.update({
+    "lay_recomp8": (LAYERED, [("constexpr int kRecompDeg = 12;", "constexpr int kRecompDeg = 8;")]),
+    "lay_recomp5": (LAYERED, [("constexpr int kRecompDeg = 12;", "constexpr int kRecompDeg = 5;")]),
+    "lay_nlr12": (LAYERED, [("constexpr int lds_rows() { return BG == 1 ? 11 : 18; }",
+                             "constexpr int lds_rows() { return BG == 1 ? 12 : 18; }")]),
+    "lay_nlr10": (LAYERED, [("constexpr int lds_rows() { return BG == 1 ? 11 : 18; }",
+                             "constexpr int lds_rows() { return BG == 1 ? 10 : 18; }")]),
+})
+
 
 def _pre(n):
     """Rotated-address table lookups of the next row group's first row (its first n core edges)
