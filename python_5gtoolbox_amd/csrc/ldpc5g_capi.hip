@@ -120,7 +120,8 @@ namespace {
 // Mixed-batch plan layout (host bytes, copied verbatim to the device):
 //   MixedPlanHdr | DecWork[nw1] (BG1) | DecWork[nw2] (BG2) | CbRef[nref]
 struct MixedPlanHdr {
-    int32_t magic, schedule, nw1, nw2, nref, pad;
+    int32_t magic, schedule, nw1, nw2, nref;
+    int32_t nz1;   // the last nz1 BG1 work items: Zc = 384 with a full G (the Zc = 384 kernels)
 };
 constexpr int32_t kPlanMagic = 0x4c504d58;   // "XMPL"
 
@@ -139,26 +140,33 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
     }
     std::vector<DecWork> work[2];
     std::vector<CbRef> refs;
+    int nz1 = 0;
     for (int g = 0; g < 2; ++g)
         for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
             const std::vector<int>& v = bucket[g][zi];
             const int Zc = kLdpcZcList[zi], G = dec_G(Zc, schedule == LDPC5G_LAYERED);
-            for (size_t s = 0; s < v.size(); s += G) {
+            // a partial workgroup first, then the full ones: for BG1 Zc = 384 (the last bucket)
+            // the full ones are the tail of the BG1 list, launched with the Zc = 384 kernel
+            const size_t part = v.size() % G;
+            auto emit = [&](size_t s, int n) {
                 DecWork w;
-                w.zi = zi, w.Zc = Zc, w.G = (int)std::min<size_t>(G, v.size() - s), w.first = (int)refs.size();
-                for (int c = 0; c < w.G; ++c) {
+                w.zi = zi, w.Zc = Zc, w.G = n, w.first = (int)refs.size();
+                for (int c = 0; c < n; ++c) {
                     CbRef r;
                     r.llr_off = desc[v[s + c]].llr_off, r.ck_off = desc[v[s + c]].ck_off, r.out = v[s + c], r.pad = 0;
                     refs.push_back(r);
                 }
                 work[g].push_back(w);
-            }
+            };
+            if (part) emit(0, (int)part);
+            for (size_t s = part; s < v.size(); s += G) emit(s, G);
+            if (g == 0 && Zc == 384) nz1 = (int)((v.size() - part) / G);
         }
     const int64_t need = (int64_t)sizeof(MixedPlanHdr) + (int64_t)(work[0].size() + work[1].size()) * (int64_t)sizeof(DecWork) +
                          (int64_t)refs.size() * (int64_t)sizeof(CbRef);
     if (!out || cap < need) return need;
     unsigned char* p = (unsigned char*)out;
-    MixedPlanHdr h{kPlanMagic, schedule, (int32_t)work[0].size(), (int32_t)work[1].size(), (int32_t)refs.size(), 0};
+    MixedPlanHdr h{kPlanMagic, schedule, (int32_t)work[0].size(), (int32_t)work[1].size(), (int32_t)refs.size(), nz1};
     memcpy(p, &h, sizeof h);
     p += sizeof h;
     for (int g = 0; g < 2; ++g) {
@@ -177,12 +185,23 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     const DecWork* w2 = w1 + h.nw1;
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
     const bool lay = h.schedule == LDPC5G_LAYERED;
+    // BG1's Zc = 384 work items (the tail of its list) run the Zc = 384 kernels, where they exist
+    // (layered float32; flooding float64) — as their own launch, so only when they fill the GPU on
+    // their own (>= 2 workgroups per CU of the MI355X's 256): a smaller set stays in the shared
+    // launch, where it overlaps the other lifting sizes (config 4's 171 workgroups measured 1.04 ->
+    // 1.17 ms split off)
+    constexpr int kZcSplitMin = 512;
+    const int nz = (lay || llr_dtype == LDPC5G_F64) && h.nz1 >= kZcSplitMin ? std::min(h.nz1, h.nw1) : 0;
     for (int g = 0; g < 2; ++g) {
-        const int nwg = g == 0 ? h.nw1 : h.nw2;
-        if (!nwg) continue;
-        if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
-                                      g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, st))
-            return rc;
+        const int nwg = g == 0 ? h.nw1 - nz : h.nw2;
+        if (nwg > 0)
+            if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
+                                          g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, st))
+                return rc;
+        if (g == 0 && nz > 0)
+            if (int rc = launch_dec_mixed(1, llr_dtype, lay, llr_base, ck_base, status, iters, nz,
+                                          w1 + (h.nw1 - nz), r, L, alpha, beta, pc, dead, st, true))
+                return rc;
     }
     return LDPC5G_OK;
 }

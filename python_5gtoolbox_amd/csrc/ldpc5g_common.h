@@ -143,13 +143,13 @@ int launch_dec_l_dead(int bgn, const float* llr, int8_t* ck, uint8_t* status, in
                       int pc, hipStream_t st);
 int launch_dec_mixed_l_dead(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                             int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
-                            double beta, int pc, hipStream_t st);
+                            double beta, int pc, hipStream_t st, bool zc384 = false);
 int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
                       int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
                       double alpha, double beta, int pc, hipStream_t st);
 int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
                             int32_t* iters, int nwg, const DecWork* work, const CbRef* cbs, int L,
-                            double alpha, double beta, int pc, hipStream_t st);
+                            double alpha, double beta, int pc, hipStream_t st, bool zc384 = false);
 int launch_flood_small(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int B, int Zc, int zi, int G, int64_t ldl, int64_t ldc, int L, double alpha,
                        double beta, int pc, hipStream_t st);
@@ -171,14 +171,14 @@ int launch_flood_mixed_dead_f32(int bgn, const float* llr, int8_t* ck, uint8_t* 
                                 hipStream_t st);
 int launch_dec_mixed_l(int bgn, const float* llr, int8_t* ck, uint8_t* status, int32_t* iters,
                        int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
-                       double beta, int pc, hipStream_t st);
+                       double beta, int pc, hipStream_t st, bool zc384 = false);
 int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, uint8_t* status,
                int32_t* iters, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L,
                double alpha, double beta, int pc, bool dead, hipStream_t st);
 int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
                      uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
                      const CbRef* cbs, int L, double alpha, double beta, int pc, bool dead,
-                     hipStream_t st);
+                     hipStream_t st, bool zc384 = false);
 int launch_bf(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
               int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc, hipStream_t st);
 int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

@@ -33,13 +33,15 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
 int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* ck,
                      uint8_t* status, int32_t* iters, int nwg, const DecWork* work,
                      const CbRef* cbs, int L, double alpha, double beta, int pc, bool dead,
-                     hipStream_t st) {
+                     hipStream_t st, bool zc384) {
     if (layered)
-        return dead ? launch_dec_mixed_l_dead(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
-                    : launch_dec_mixed_l(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
-    if (dead) return launch_flood_mixed_dead(bgn, dtype, llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+        return dead ? launch_dec_mixed_l_dead(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st, zc384)
+                    : launch_dec_mixed_l(bgn, (const float*)llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st, zc384);
+    if (dead) return launch_flood_mixed_dead(bgn, dtype, llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st, zc384);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
+        if (zc384 && bgn == 1)
+            return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }

@@ -921,14 +921,15 @@ int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int 
                                                   beta, pc, st);
 }
 
-template <int BG, typename T, bool LAYERED, bool DEAD = false>
+// ZCC > 0: every work item is a Zc = ZCC item with a full G (ldpc5g_capi.hip build_plan puts them last)
+template <int BG, typename T, bool LAYERED, bool DEAD = false, int ZCC = 0>
 int launch_dec_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
                        const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                        int pc, hipStream_t st) {
-    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD>() : dec_kernel<BG, T, LAYERED, false, DEAD>();
+    auto kern = beta != 0.0 ? dec_kernel<BG, T, LAYERED, true, DEAD, ZCC>() : dec_kernel<BG, T, LAYERED, false, DEAD, ZCC>();
     const size_t lds = dec_lds_bytes<BG, T, LAYERED>();
-    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD>()>(lds)
-                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD>()>(lds))
+    if (int rc = beta != 0.0 ? set_lds_once<dec_kernel<BG, T, LAYERED, true, DEAD, ZCC>()>(lds)
+                             : set_lds_once<dec_kernel<BG, T, LAYERED, false, DEAD, ZCC>()>(lds))
         return rc;
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(dec_cs<LAYERED>()), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);

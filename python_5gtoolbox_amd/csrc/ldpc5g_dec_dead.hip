@@ -18,9 +18,11 @@ int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* 
 
 int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status,
                             int32_t* iters, int nwg, const DecWork* work, const CbRef* cbs, int L,
-                            double alpha, double beta, int pc, hipStream_t st) {
+                            double alpha, double beta, int pc, hipStream_t st, bool zc384) {
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
+        if (zc384 && bgn == 1)
+            return launch_flood_mixed_t<1, double, true, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }

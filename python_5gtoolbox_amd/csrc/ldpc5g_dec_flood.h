@@ -920,14 +920,15 @@ int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, in
                                                              alpha, beta, pc, st);
 }
 
-template <int BG, typename T, bool DEAD = false>
+// ZCC > 0: every work item is a Zc = ZCC item (G = 1; ldpc5g_capi.hip build_plan puts them last)
+template <int BG, typename T, bool DEAD = false, int ZCC = 0>
 int launch_flood_mixed_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg,
                          const DecWork* work, const CbRef* cbs, int L, double alpha, double beta,
                          int pc, hipStream_t st) {
     const bool ofs = beta != 0.0;
-    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS, DEAD>
-                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS, DEAD>;
-    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS, DEAD>(ofs)) return rc;
+    auto kern = ofs ? ldpc_flood_kernel<BG, T, true, kFloodNP, kFloodCS, DEAD, ZCC>
+                    : ldpc_flood_kernel<BG, T, false, kFloodNP, kFloodCS, DEAD, ZCC>;
+    if (int rc = set_flood_lds<BG, T, kFloodNP, kFloodCS, DEAD, ZCC>(ofs)) return rc;
     const size_t lds = flood_lds_bytes<BG, T, kFloodNP, kFloodCS>();
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFloodNP * kFloodCS), lds, st, llr, ck, status, iters, 0, 0,
                        0, 0, (int64_t)0, (int64_t)0, L, (T)alpha, (T)beta, pc, work, cbs);

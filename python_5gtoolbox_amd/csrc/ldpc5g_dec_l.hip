@@ -17,7 +17,9 @@ int launch_dec_l(int bgn, const float* p, int8_t* ck, uint8_t* status, int32_t* 
 
 int launch_dec_mixed_l(int bgn, const float* p, int8_t* ck, uint8_t* status, int32_t* iters,
                        int nwg, const DecWork* work, const CbRef* cbs, int L, double alpha,
-                       double beta, int pc, hipStream_t st) {
+                       double beta, int pc, hipStream_t st, bool zc384) {
+    if (zc384 && bgn == 1)
+        return launch_dec_mixed_t<1, float, true, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     return bgn == 1 ? launch_dec_mixed_t<1, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                     : launch_dec_mixed_t<2, float, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
 }

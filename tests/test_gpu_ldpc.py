@@ -309,12 +309,39 @@ def test_decode_mixed_batch(torch):
                 items.append((bg, Zc, llr[k]))
     order = rng.permutation(len(items))
     items = [items[i] for i in order]
-    for schedule in ("flooding", "layered"):
-        outs, st, it = MX.decode_mixed([(b, z, l) for b, z, l in items], 8, 1.0, 0.5, schedule)
+    # (5 BG1 Zc=384 codeblocks: a partial and two full layered workgroups, the full ones through
+    # the Zc = 384 kernel; float64 flooding: all five through it)
+    for schedule, dt in (("flooding", np.float32), ("layered", np.float32), ("flooding", np.float64)):
+        outs, st, it = MX.decode_mixed([(b, z, l.astype(dt)) for b, z, l in items], 8, 1.0, 0.5, schedule)
         for k, (bg, Zc, llr) in enumerate(items):
             ref = (O.decode_layered(llr[None], Zc, bg, 8, 1.0, 0.5) if schedule == "layered"
-                   else O.decode_flooding(llr[None], Zc, bg, 8, 1.0, 0.5, np.float32))
+                   else O.decode_flooding(llr[None].astype(dt), Zc, bg, 8, 1.0, 0.5, dt))
             assert np.array_equal(outs[k], ref[0][0]) and st[k] == ref[1][0] and it[k] == ref[2][0]
+
+
+@pytest.mark.parametrize("schedule,dt,n384", [("layered", np.float32, 1031), ("flooding", np.float64, 515)])
+def test_decode_mixed_batch_zc384_launch(torch, dec, schedule, dt, n384):
+    """A mixed call with enough BG1 Zc=384 codeblocks (>= 512 workgroups) for their own launch of
+    the Zc = 384 kernel (ldpc5g_capi.hip launch_plan): every codeblock identical to the uniform
+    batch decode of its (bg, Zc), itself bit-exact with the oracle (test_decode_z384_*)."""
+    from python_5gtoolbox_amd import nr_ldpc_decode_mixed as MX
+    rng = np.random.default_rng(n384)
+    groups = {(1, 384): n384, (2, 52): 9}
+    items, llrs = [], {}
+    for (bg, Zc), n in groups.items():
+        K = (22 if bg == 1 else 10) * Zc
+        dn = O.encode(rng.integers(0, 2, (n, K)).astype(np.int8), bg)
+        llr = O.bpsk_awgn_llr(dn, float(rng.uniform(0, 1.5)), rng).astype(dt)
+        llrs[(bg, Zc)] = llr
+        items += [(bg, Zc, k) for k in range(n)]
+    order = rng.permutation(len(items))
+    items = [items[i] for i in order]
+    outs, st, it = MX.decode_mixed([(b, z, llrs[(b, z)][k]) for b, z, k in items], 8, 1.0, 0.5, schedule)
+    ref = {key: dec.nr_decode_ldpc_batch(v, key[1], key[0], 8, "min-sum", 1.0, 0.5, schedule)
+           for key, v in llrs.items()}
+    for j, (bg, Zc, k) in enumerate(items):
+        rck, rst, rit = ref[(bg, Zc)]
+        assert np.array_equal(outs[j], rck[k]) and st[j] == rst[k] and it[j] == rit[k]
 
 
 def test_decode_errors_are_assertions(torch, dec):

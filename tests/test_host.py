@@ -195,13 +195,18 @@ def test_mixed_plan_built_on_host():
     for k in range(8):
         d[k].bgn, d[k].Zc = (1, 384) if k < 5 else (2, 12)
         d[k].llr_off, d[k].ck_off = 1000 * k, 2000 * k
-    for sched, nw1, nw2 in ((_lib.LAYERED, 3, 1), (_lib.FLOODING, 5, 1)):
+    for sched, nw1, nw2, nz1 in ((_lib.LAYERED, 3, 1, 2), (_lib.FLOODING, 5, 1, 5)):
         n = lib.ldpc5g_mixed_plan(d, 8, sched, None, 0)
         assert n == 24 + 16 * (nw1 + nw2) + 24 * 8
         buf = (ctypes.c_ubyte * n)()
         assert lib.ldpc5g_mixed_plan(d, 8, sched, buf, n) == n
         hdr = np.frombuffer(bytes(buf)[:24], np.int32)
         assert hdr[1] == sched and hdr[2] == nw1 and hdr[3] == nw2 and hdr[4] == 8
+        # the BG1 Zc=384 items: a partial workgroup first, then the nz1 full ones (the Zc = 384
+        # kernels' share, launched last)
+        assert hdr[5] == nz1
+        work = np.frombuffer(bytes(buf)[24:24 + 16 * nw1], np.int32).reshape(nw1, 4)
+        assert list(work[:, 2]) == ([1, 2, 2] if sched == _lib.LAYERED else [1] * 5)
     d[3].Zc = 383
     assert lib.ldpc5g_mixed_plan(d, 8, _lib.LAYERED, None, 0) == _lib.EZC
     assert lib.ldpc5g_decode_ms_mixed_plan(None, None, None, 1, None, None, None, 8, 1.0, 0.0,
