@@ -40,18 +40,8 @@ constexpr int kXPre = LDPC5G_FLOOD_XPRE;
 #define LDPC5G_FLOOD_ASB 1
 #endif
 constexpr int kAPre = LDPC5G_FLOOD_APRE;
-// phase B: edge k's sign bit by one shift of the row's sign word (u << k) per edge it adds, instead
-// of shifting the word once per edge of the row (the LDS rows' halves add alternate edges)
-// phase A: a part's rows processed two at a time with their edges interleaved (two independent
-// dependency chains per wave between the per-edge volatile asm points), non-DEAD kernels only
-#ifndef LDPC5G_FLOOD_PAIR
-#define LDPC5G_FLOOD_PAIR 0
-#endif
-constexpr bool kPair = LDPC5G_FLOOD_PAIR != 0;
-#ifndef LDPC5G_FLOOD_BSHIFT
-#define LDPC5G_FLOOD_BSHIFT 0
-#endif
-constexpr bool kBShift = LDPC5G_FLOOD_BSHIFT != 0;
+// (variants measured and dropped — rows of a part paired with interleaved edges, phase-B sign words
+// shifted per added edge, phase-B table offsets, sign-word syndrome parity: DESIGN.md §4.2b)
 constexpr bool kASb = LDPC5G_FLOOD_ASB != 0;
 // phase A takes its rotated core-edge offsets from an LDS wrap table (one LDS read issued two edges
 // ahead instead of the add/add/min arithmetic: 3 half-rate VALU ops per edge) in the float64 BG1
@@ -81,8 +71,6 @@ struct FloodPlan {
     int xpos[64] = {};        // rank of ext row i (i >= 4) among its owner part's ext rows
     int xlist[NP][64] = {};   // ext rows of each part, ascending
     int nx[NP] = {};
-    int rlist[NP][64] = {};   // rows of each part (phase A owner), ascending
-    int nr[NP] = {};
     static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
     constexpr FloodPlan() {
         using P = BGT<BG>;
@@ -141,7 +129,6 @@ struct FloodPlan {
             xpos[i] = nx[owner[i]];
             xlist[owner[i]][nx[owner[i]]++] = i;
         }
-        for (int i = 0; i < P::MB; ++i) rlist[owner[i]][nr[owner[i]]++] = i;
         for (int j = 0; j < P::KC; ++j) {
             first_row[j] = -1;
             for (int i = 0; i < P::MB && first_row[j] < 0; ++i)
@@ -558,20 +545,6 @@ __device__ __forceinline__ void flood_body(
             sfor<0, d>([&](auto kc) { rstep(r, ic, kc); });
             rend(r, ic);
         };
-        // two rows with their edges interleaved (edge k of A, then edge k of B)
-        auto rowA2 = [&](auto ica, auto icb) {
-            constexpr int da = P::RS[decltype(ica)::value + 1] - P::RS[decltype(ica)::value];
-            constexpr int db = P::RS[decltype(icb)::value + 1] - P::RS[decltype(icb)::value];
-            RowSt ra, rb;
-            rbegin(ra, ica);
-            rbegin(rb, icb);
-            sfor<0, (da > db ? da : db)>([&](auto kc) {
-                if constexpr (decltype(kc)::value < da) rstep(ra, ica, kc);
-                if constexpr (decltype(kc)::value < db) rstep(rb, icb, kc);
-            });
-            rend(ra, ica);
-            rend(rb, icb);
-        };
         // dead extension row: LQ_ext = 0 + r_old_ext (its syndrome bit), q_core = LQ - (+-0);
         // new state as the full update leaves it up to zero signs: nA = 0, nB = alpha * max(
         // min |q_core| - beta, 0), argmin = the extension edge, whose sign bit is the row sign
@@ -612,35 +585,17 @@ __device__ __forceinline__ void flood_body(
         };
         if (active) {
             per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
-            if constexpr (kPair && !DEAD) {
-                // each part's rows in pairs, one pair per scheduling region
-                per_half([&](auto hc) {
-                    constexpr int hh = decltype(hc)::value, nr = kFloodPlan<BG, T, NP, CS>.nr[hh];
-                    sfor<0, (nr + 1) / 2>([&](auto pc2) {
-                        constexpr int x = 2 * decltype(pc2)::value;
-                        constexpr int ia = kFloodPlan<BG, T, NP, CS>.rlist[hh][x];
-                        if constexpr (x + 1 < nr) {
-                            constexpr int ib = kFloodPlan<BG, T, NP, CS>.rlist[hh][x + 1];
-                            rowA2(std::integral_constant<int, ia>{}, std::integral_constant<int, ib>{});
-                        } else {
-                            rowA(std::integral_constant<int, ia>{});
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                    });
-                });
-            } else {
-                sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
-                    constexpr int i = decltype(ic)::value;
-                    if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
-                        if constexpr (DEAD && i >= 4) {
-                            if (rdead(ic)) rowA_dead(ic);
-                            else rowA(ic);
-                        } else {
-                            rowA(ic);
-                        }
+            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
+                constexpr int i = decltype(ic)::value;
+                if (h == kFloodPlan<BG, T, NP, CS>.owner[i]) {
+                    if constexpr (DEAD && i >= 4) {
+                        if (rdead(ic)) rowA_dead(ic);
+                        else rowA(ic);
+                    } else {
+                        rowA(ic);
                     }
-                });
-            }
+                }
+            });
             if (fail) flagA[cl] = 1;
         }
         // phase B's shift words are loaded one row group ahead (scalar loads issued before the
@@ -689,7 +644,7 @@ __device__ __forceinline__ void flood_body(
                     return n;
                 }();
                 if constexpr (j < KC && (split < 0 || cidx % NP == split)) {
-                    const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), kBShift ? u << k : u, mv);
+                    const T r = xsign_v(pick(idxn == (uint32_t)k, nB, nA), u, mv);
                     lds_T& acc = at(j * CS * TS + rot(gshift(e0 + k)));
                     if constexpr (kFloodPlan<BG, T, NP, CS>.first_row[j] == i) {
                         acc = T(0) + r;
@@ -703,7 +658,7 @@ __device__ __forceinline__ void flood_body(
                         acc = acc + r;
                     }
                 }
-                if constexpr (!kBShift) asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
+                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
             });
         };
         // the core LLRs of the LQ update, loaded now so phase B hides their latency

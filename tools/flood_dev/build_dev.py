@@ -41,20 +41,12 @@ VARIANTS = {
 
 # compile-time flags per variant (the product header's LDPC5G_FLOOD_* knobs)
 FLAGS = {
-    "pre0": ["-DLDPC5G_FLOOD_APRE=0", "-DLDPC5G_FLOOD_ASB=0"],
-    "pre0bs": ["-DLDPC5G_FLOOD_APRE=0", "-DLDPC5G_FLOOD_ASB=0", "-DLDPC5G_FLOOD_BSHIFT=1"],
     "pre1": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=0"],
     "pre2": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=0"],
     "pre3": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=0"],
     "pre1sb": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=1"],
     "pre2sb": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=1"],
     "pre3sb": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=1"],
-    "bshift": ["-DLDPC5G_FLOOD_BSHIFT=1"],
-    "pre1sbbs": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=1", "-DLDPC5G_FLOOD_BSHIFT=1"],
-    "pre2bs": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_BSHIFT=1"],
-    "pair": ["-DLDPC5G_FLOOD_PAIR=1"],
-    "pair_nosb": ["-DLDPC5G_FLOOD_PAIR=1", "-DLDPC5G_FLOOD_ASB=0"],
-    "pair_pre0": ["-DLDPC5G_FLOOD_PAIR=1", "-DLDPC5G_FLOOD_APRE=0", "-DLDPC5G_FLOOD_ASB=0"],
 }
 for _n in FLAGS:
     VARIANTS.setdefault(_n, [])
