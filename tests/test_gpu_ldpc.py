@@ -214,25 +214,26 @@ def test_decode_z384_batch_vs_oracle(torch, dec, schedule, dtype):
         assert np.array_equal(g, r)
 
 
-@pytest.mark.parametrize("schedule,dtype,rm", [("layered", np.float32, False), ("layered", np.float32, True),
-                                               ("flooding", np.float64, False), ("flooding", np.float64, True)])
-def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm):
+@pytest.mark.parametrize("schedule,dtype,rm,bg", [("layered", np.float32, False, 1), ("layered", np.float32, True, 1),
+                                                  ("flooding", np.float64, False, 1), ("flooding", np.float64, True, 1),
+                                                  ("flooding", np.float64, False, 2), ("flooding", np.float64, True, 2)])
+def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
     """The Zc = 384 kernels (lifting size and shifts compile-time, wrap-table offsets as immediates):
     offset min-sum (beta > 0), an odd batch (a half-empty last workgroup of the layered kernel),
     mixed SNRs, and rate-matched rows (untransmitted extension columns +0.0: the dead-row
     variants), bit-exact with the oracle."""
-    rng = np.random.default_rng(7 + rm)
+    rng = np.random.default_rng(7 + rm + 10 * bg)
     Zc, B = 384, 7
-    ck = rng.integers(0, 2, (B, 22 * Zc)).astype(np.int8)
-    dn = O.encode(ck, 1)
+    ck = rng.integers(0, 2, (B, (22 if bg == 1 else 10) * Zc)).astype(np.int8)
+    dn = O.encode(ck, bg)
     snr = rng.choice([-1.0, 1.0, 3.0], size=B)[:, None]
     llr = (2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) /
            10 ** (-snr / 10)).astype(dtype)
     if rm:   # the last 20 extension columns never transmitted
         llr[:, -20 * Zc:] = 0
-    got = dec.nr_decode_ldpc_batch(llr, Zc, 1, 6, "min-sum", 1.0, 0.5, schedule, rate_matched=rm)
-    ref = (O.decode_layered(llr, Zc, 1, 6, 1.0, 0.5) if schedule == "layered"
-           else O.decode_flooding(llr, Zc, 1, 6, 1.0, 0.5, dtype))
+    got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 6, "min-sum", 1.0, 0.5, schedule, rate_matched=rm)
+    ref = (O.decode_layered(llr, Zc, bg, 6, 1.0, 0.5) if schedule == "layered"
+           else O.decode_flooding(llr, Zc, bg, 6, 1.0, 0.5, dtype))
     for g, r in zip(got, ref):
         assert np.array_equal(g, r)
 
