@@ -44,13 +44,14 @@ constexpr int kAPre = LDPC5G_FLOOD_APRE;
 // shifted per added edge, phase-B table offsets, sign-word syndrome parity: DESIGN.md §4.2b)
 constexpr bool kASb = LDPC5G_FLOOD_ASB != 0;
 // phase A takes its rotated core-edge offsets from an LDS wrap table (one LDS read issued two edges
-// ahead instead of the add/add/min arithmetic: 3 half-rate VALU ops per edge) in the float64 batch
-// kernels, whose LDS has room for it (2 x 384 u32 entries; the state rows still number 10 for
-// BG1, 11 for BG2; BG2 Zc=384 2.97 -> 2.78 ms per 4096 codeblocks).
+// ahead instead of the add/add/min arithmetic: 3 half-rate VALU ops per edge) in the batch
+// kernels (2 parts x 384 slots), whose LDS has room for it (2 x 384 u32 entries; the numbers of
+// LDS state rows do not change; float64 BG2 Zc=384 2.97 -> 2.78 ms per 4096 codeblocks, float32
+// BG1 Zc=384 1.18 -> 1.31 M CB/s).
 // r04: 4.04 -> 3.93 ms per 4096 codeblocks.  (Phase B keeps the arithmetic: a table read there
 // adds an LDS round trip to each barrier-separated row group, measured 4.08 ms.)
 template <int BG, typename T, int NP, int CS>
-constexpr bool flood_wtab() { return sizeof(T) == 8 && NP == 2 && CS == 384; }
+constexpr bool flood_wtab() { return NP == 2 && CS == 384; }
 template <int BG, typename T, int NP, int CS>
 constexpr int flood_wtab_bytes() { return flood_wtab<BG, T, NP, CS>() ? 2 * CS * 4 : 0; }
 // ZCC > 0 (zc_shift, ldpc5g_dec_body.h): a kernel for the one lifting size Zc = 384 = CS, one
