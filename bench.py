@@ -41,7 +41,7 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 # both kernels is DEAD, the LDPC5G_RATE_MATCHED variant, false for the headline; then the
 # compile-time lifting size, 384 for the Zc = 384 kernels, 0 for the runtime-Zc ones)
 DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false, false, 384>",
-              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false, 0>"}
+              "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false, 384>"}
 DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384, false, 384>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
