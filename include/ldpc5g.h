@@ -84,8 +84,9 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
  * bgn), called one codeblock at a time by the reference's callers (nr_dlsch_decode.py:91,
  * scripts/internal/sim_ldpc_internal.py:50-58).  float64 flooding min-sum (bit-exact with the
  * reference) / the encoder on B contiguous host rows (llr [B][N or Nf], ck [B][Nf], status [B],
- * iters [B]; ck [B][K], dn [B][N]): the rows go through a per-thread pinned staging buffer and a
- * per-thread device buffer (grown on demand and held for the life of the process), one H2D copy,
+ * iters [B]; ck [B][K], dn [B][N]): the rows go through a pinned staging buffer and a device
+ * buffer kept per thread AND per device ordinal (< 64; grown on demand and held for the life of
+ * the process, so a thread that alternates devices reuses each device's pair), one H2D copy,
  * the kernel, one D2H copy and one synchronisation of `stream` — no caller-side device memory.
  * Synchronous: returns when the outputs are written.  beta < 0 is rejected (see decode_sparse). */
 int ldpc5g_decode_ms_host(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

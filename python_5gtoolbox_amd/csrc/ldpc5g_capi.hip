@@ -185,8 +185,9 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     const DecWork* w2 = w1 + h.nw1;
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
     const bool lay = h.schedule == LDPC5G_LAYERED;
-    // BG1's Zc = 384 work items (the tail of its list) run the Zc = 384 kernels, where they exist
-    // (layered float32; flooding float64) — as their own launch, so only when they fill the GPU on
+    // BG1's Zc = 384 work items (the tail of its list) run the Zc = 384 kernels of mixed plans
+    // (layered float32, flooding float64; a mixed plan's float32 flooding items and BG2 items keep the
+    // generic kernels, although launch_flood_t has Zc = 384 kernels for those too) — as their own launch, so only when they fill the GPU on
     // their own (>= 2 workgroups per CU of the MI355X's 256): a smaller set stays in the shared
     // launch, where it overlaps the other lifting sizes (config 4's 171 workgroups measured 1.04 ->
     // 1.17 ms split off)
@@ -275,22 +276,23 @@ int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
 
 namespace ldpc5g_impl {
 namespace {
-// Per-thread device + pinned buffers of the host-buffer entry points (grown on demand, never freed:
-// a thread-exit destructor could run after the HIP runtime is gone; include/ldpc5g.h states it).
+// Per-thread device + pinned buffers of the host-buffer entry points, one set per device ordinal
+// (a thread that alternates devices keeps and reuses each device's set; grown on demand, never
+// freed: a thread-exit destructor could run after the HIP runtime is gone; include/ldpc5g.h states it).
 struct HostStage {
     void* dev = nullptr;
     size_t dcap = 0;
     void* pin = nullptr;
     size_t pcap = 0;
-    int device = -1;
 };
-thread_local HostStage t_hs;
+constexpr int kMaxStageDevices = 64;
+thread_local HostStage t_hs[kMaxStageDevices];
 
 int host_stage(size_t bytes, unsigned char** d, unsigned char** p) {
     int dev = 0;
     if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
-    HostStage& h = t_hs;
-    if (h.device != dev) h = HostStage{}, h.device = dev;   // buffers of another device stay alive
+    if (dev < 0 || dev >= kMaxStageDevices) return fail(LDPC5G_ESIZE, "device ordinal %d >= %d", dev, kMaxStageDevices);
+    HostStage& h = t_hs[dev];
     if (h.dcap < bytes) {
         if (h.dev) (void)hipFree(h.dev);
         h.dev = nullptr, h.dcap = 0;
@@ -305,6 +307,12 @@ int host_stage(size_t bytes, unsigned char** d, unsigned char** p) {
     }
     *d = (unsigned char*)h.dev, *p = (unsigned char*)h.pin;
     return LDPC5G_OK;
+}
+// an error after the first copy was queued: drain the stream before returning, so the next call
+// on this thread never rewrites (or frees) a pinned buffer a queued copy may still be reading
+int drained(int rc, hipStream_t st) {
+    if (rc) (void)hipStreamSynchronize(st);
+    return rc;
 }
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 }  // namespace
@@ -330,12 +338,12 @@ int ldpc5g_decode_ms_host(const double* llr, int8_t* ck, uint8_t* status, int32_
     if (int rc = host_stage(total, &d, &p)) return rc;
     hipStream_t st = (hipStream_t)stream;
     memcpy(p, llr, nin);
-    if (int rc = check_hip(hipMemcpyAsync(d, p, nin, hipMemcpyHostToDevice, st), "hipMemcpyAsync(llr)")) return rc;
+    if (int rc = check_hip(hipMemcpyAsync(d, p, nin, hipMemcpyHostToDevice, st), "hipMemcpyAsync(llr)")) return drained(rc, st);
     if (int rc = launch_dec(bgn, LDPC5G_F64, false, d, (int8_t*)(d + o_ck), d + o_st, (int32_t*)(d + o_it), B, Zc, zi,
                             N, Nf, L, alpha, beta, pc, (flags & LDPC5G_RATE_MATCHED) != 0, st))
-        return rc;
+        return drained(rc, st);
     if (int rc = check_hip(hipMemcpyAsync(p + o_ck, d + o_ck, total - o_ck, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(out)"))
-        return rc;
+        return drained(rc, st);
     if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize")) return rc;
     memcpy(ck, p + o_ck, nck);
     memcpy(status, p + o_st, (size_t)B);
@@ -357,10 +365,10 @@ int ldpc5g_encode_host(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int
     if (int rc = host_stage(total, &d, &p)) return rc;
     hipStream_t st = (hipStream_t)stream;
     memcpy(p, ck, nk);
-    if (int rc = check_hip(hipMemcpyAsync(d, p, nk, hipMemcpyHostToDevice, st), "hipMemcpyAsync(ck)")) return rc;
-    if (int rc = launch_encode((const int8_t*)d, (int8_t*)(d + o_dn), B, bgn, Zc, zi, K, N, st)) return rc;
+    if (int rc = check_hip(hipMemcpyAsync(d, p, nk, hipMemcpyHostToDevice, st), "hipMemcpyAsync(ck)")) return drained(rc, st);
+    if (int rc = launch_encode((const int8_t*)d, (int8_t*)(d + o_dn), B, bgn, Zc, zi, K, N, st)) return drained(rc, st);
     if (int rc = check_hip(hipMemcpyAsync(p + o_dn, d + o_dn, (size_t)B * N, hipMemcpyDeviceToHost, st), "hipMemcpyAsync(dn)"))
-        return rc;
+        return drained(rc, st);
     if (int rc = check_hip(hipStreamSynchronize(st), "hipStreamSynchronize")) return rc;
     memcpy(dn, p + o_dn, (size_t)B * N);
     return LDPC5G_OK;

@@ -14,8 +14,10 @@
 //     slots whose reads are all independent; the edge words (column, CSC slot, V mod Zc) are staged
 //     into LDS once per launch, a thread per edge (lane-varying rows read them by LDS broadcast), and
 //     a row's LQ reads are issued 8 at a time before any is used.
-// LDS: LQ of the core columns + one message per core edge, KC*Zc + Ec*Zc values (BG1 Zc=64 float64:
-// 153.6 KB of the CU's 160 KB).
+// LDS (small_lds_bytes_t): the doubled LQ of the core columns, the +inf / discard / zero rows and one
+// message per core edge, (2*KC + 2 + Ec + 2)*Zc values, plus the edge words: 2,640*Zc + 7,008 B for
+// BG1 float64, so the largest BG1 float64 lifting size that fits the CU's 160 KB is Zc = 56 (154.8 KB;
+// BG1 float64 Zc = 60 / 64 run the batch kernel's 16-part configuration instead).
 #pragma once
 #include "ldpc5g_dec_flood.h"
 

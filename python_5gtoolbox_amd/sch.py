@@ -191,12 +191,16 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
     assert algo in ["BF", "BP", "min-sum"]
     T = llr.shape[0]
     ws = ws or SchWorkspace(cfg, T, llr.device)
-    dn_dtype = dn_dtype or (t.float32 if schedule == "layered" else llr.dtype)
     if algo == "min-sum" and not beta >= 0:
         # the reference decodes each codeblock with nr_decode_ldpc (nr_dlsch_decode.py:91,
         # nr_ulsch_decode.py:92), which keeps min-sum's literal zero branches for beta < 0
-        # (nr_ldpc_decode.py:186-225): the sparse kernel on the base graph, as nr_decode_ldpc here
+        # (nr_ldpc_decode.py:186-225): the float64 sparse flooding kernel on the base graph, as
+        # nr_decode_ldpc here.  beta < 0 therefore always runs the reference's float64 flooding
+        # chain: a layered schedule or a float32 dn_dtype is refused, not silently ignored.
         from .nr_ldpc_decode import SparseGraph, _sparse_graph, decode_ldpc_batch
+        assert schedule == "flooding", "beta < 0 decodes with the float64 flooding sparse kernel only"
+        assert dn_dtype in (None, t.float64), "beta < 0: rate recovery must be float64 (dn_dtype)"
+        dn_dtype = t.float64
         llr_dn = sch_raterecover_batch(llr, cfg, harq_in, dn_dtype, ws)
         x = t.zeros((T * cfg.C, cfg.N + 2 * cfg.Zc), dtype=t.float64, device=llr.device)
         x[:, 2 * cfg.Zc:] = llr_dn   # punctured systematic columns: LLR 0 (nr_ldpc_decode.py:43)
@@ -205,6 +209,7 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
         decode_ldpc_batch(x, g, L, algo, alpha, beta, out=(ws.dec_ck, ws.status, ws.iters))
         sch_tb_check_batch(ws.dec_ck, cfg, T, ws)
     elif algo == "min-sum":
+        dn_dtype = dn_dtype or (t.float32 if schedule == "layered" else llr.dtype)
         out = ws.dn_buf(dn_dtype, cfg)
         if harq_in is not None:
             assert harq_in.dtype == dn_dtype and harq_in.shape == out.shape and harq_in.is_contiguous()
@@ -221,6 +226,7 @@ def sch_decode_batch(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule=
         llr_dn = out
     else:
         from .nr_ldpc_decode import nr_decode_ldpc_batch
+        dn_dtype = dn_dtype or (t.float32 if schedule == "layered" else llr.dtype)
         llr_dn = sch_raterecover_batch(llr, cfg, harq_in, dn_dtype, ws)
         nr_decode_ldpc_batch(llr_dn, cfg.Zc, cfg.bgn, L, algo, alpha, beta, "flooding",
                              out=(ws.dec_ck, ws.status, ws.iters), rate_matched=True)

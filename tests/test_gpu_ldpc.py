@@ -173,12 +173,15 @@ def test_decode_flooding_small_launch(torch, dec, bg, Zc, B, dtype):
         assert np.array_equal(g, r)
 
 
-@pytest.mark.parametrize("bg,Zc,B", [(1, 64, 1), (2, 64, 1), (2, 8, 8), (1, 2, 32), (1, 40, 1)])
+@pytest.mark.parametrize("bg,Zc,B", [(1, 64, 1), (2, 64, 1), (2, 8, 8), (1, 2, 32), (1, 40, 1), (1, 48, 1),
+                                     (1, 56, 1)])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_decode_small_kernel_edge_cases(torch, dec, bg, Zc, B, dtype):
     """The small-codeblock kernel (ldpc5g_dec_small.h, B * Zc <= 64) on its edge cases, bit-exact
     with the oracle: NMS (beta 0) and OMS, L = 0 / 1 / 8, integer LLRs (|q| ties, argmin order),
-    an all-zero codeblock and a noiseless one (exit at iteration 0)."""
+    an all-zero codeblock and a noiseless one (exit at iteration 0).  BG1 Zc = 48 / 56 are the
+    three-nodes-per-thread (RPT = 3) instantiation; Zc = 56 is the largest BG1 float64 lifting size
+    whose LDS fits, so BG1 Zc = 64 float64 exercises the 16-part fallback (small_fits false)."""
     rng = np.random.default_rng(Zc * 7 + B)
     K = (22 if bg == 1 else 10) * Zc
     ck = rng.integers(0, 2, (B, K)).astype(np.int8)

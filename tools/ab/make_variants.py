@@ -317,8 +317,8 @@ _REDERIVE_FLAGS = [
 # (r04: lay_rederive2 = _REDERIVE + _REDERIVE_FLAGS measured 2.348 vs 2.371 ms / 8.843 vs 9.055 ms at
 #  4096 / 16384 codeblocks, 0 B/lane scratch; adopted into ldpc5g_dec_body.h, so these patches no
 #  longer apply and are kept as the record of the change)
-# unified diffs against python_5gtoolbox_amd/csrc (applied with patch -p3 in the copy)
-VARIANTS.update({"lay_bitsyn": (LAYERED, "tools/ab/bitsyn_final_syndrome.patch")})
+# (a variant may also name a unified diff against python_5gtoolbox_amd/csrc, applied with patch -p3
+#  in the copy; r04's lay_bitsyn diff was measured, rejected and deleted in r05: DESIGN.md §7)
 
 
 def make(name):

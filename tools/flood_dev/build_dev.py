@@ -25,6 +25,8 @@ VARIANTS = {
             ("                        } else if constexpr (kFloodPlan<BG, T, NP, CS>.owner[i] == decltype(hc)::value) {",
              "                        } else if constexpr (i < 0) {")],
     "nobar": [("            if (!gd) lds_barrier();\n        });", "        });")],
+    "noX": [("                xr[p % XP] = llrx(kFloodPlan<BG, T, NP, CS>.xlist[hh][p]);",
+             "                xr[p % XP] = T(1.5 + p);")],
     "plain": [("                        __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);",
                "                        acc = r;")],
     # register-pressure probes of the gather phase B (compile only)
@@ -47,6 +49,7 @@ FLAGS = {
     "pre1sb": ["-DLDPC5G_FLOOD_APRE=1", "-DLDPC5G_FLOOD_ASB=1"],
     "pre2sb": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=1"],
     "pre3sb": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=1"],
+    "nosxpop": ["-DLDPC5G_FLOOD_SXPOP=0"],
 }
 for _n in FLAGS:
     VARIANTS.setdefault(_n, [])
