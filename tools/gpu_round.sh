@@ -36,25 +36,25 @@ fi
 if has trace; then
   echo "[gpu_round] rocprof kernel trace"
   cd /tmp
-  # headline only (the bench's 3 warmup + 20 timed launches; the summary skips the warmups, so the
-  # decoder's average is over the launches behind the bench's ms_per_step)
+  # each config-3 line alone (the bench's 3 warmup + 20 timed launches; the summary skips the
+  # warmups, so the decoder's average is over the launches behind the line's ms_per_step):
+  # the headline (float64 flooding, reference-exact), then the float32 layered perf_mode line
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$OUT/prof_headline" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --no-reference \
+      -d "$OUT/prof_headline" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --no-perf \
       > "$OUT/bench_headline_under_rocprof.json" 2> "$OUT/rocprof_headline.err" || { tail -20 "$OUT/rocprof_headline.err"; die trace $?; }
-  # the reference-precision line (float64 flooding): its kernel runs only in that line
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$OUT/prof_reference" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras \
-      > "$OUT/bench_reference_under_rocprof.json" 2> "$OUT/rocprof_reference.err" || { tail -20 "$OUT/rocprof_reference.err"; die trace $?; }
+      -d "$OUT/prof_layered" -o run -- python -u "$ROOT/bench.py" --cpu-seconds 0 --no-extras --no-perf --headline layered \
+      > "$OUT/bench_layered_under_rocprof.json" 2> "$OUT/rocprof_layered.err" || { tail -20 "$OUT/rocprof_layered.err"; die trace $?; }
   # everything (extras: encoder, flooding, config 4 / 5 chains): per-kernel table
   timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python -u "$ROOT/bench.py" --steps 10 --cpu-seconds 0 > "$OUT/bench_under_rocprof.json" 2> "$OUT/rocprof.err" \
       || { tail -20 "$OUT/rocprof.err"; die trace $?; }
   cd "$ROOT"
   python tools/rocpd_summary.py "$OUT/prof_headline" --skip 3 > "$OUT/kernel_stats_headline.csv"
-  python tools/rocpd_summary.py "$OUT/prof_reference" --skip 3 > "$OUT/kernel_stats_reference.csv"
+  python tools/rocpd_summary.py "$OUT/prof_layered" --skip 3 > "$OUT/kernel_stats_layered.csv"
   python tools/rocpd_summary.py "$OUT/prof" > "$OUT/kernel_stats.csv"
   cut -c1-150 "$OUT/kernel_stats_headline.csv" | head -6
-  cut -c1-150 "$OUT/kernel_stats_reference.csv" | head -6
+  cut -c1-150 "$OUT/kernel_stats_layered.csv" | head -6
   cut -c1-150 "$OUT/kernel_stats.csv" | head -12
 fi
 if has fdev; then
