@@ -349,19 +349,22 @@ def valu_line(edges, ms):
 def bench_config4(torch, dist, world, dev, rank, steps):
     """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
     (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
-    GPU chain (encode -> rate match -> BPSK+AWGN -> rate recover), OMS beta=0.5, L=8, decoded by
-    ldpc5g_decode_ms_mixed (one call, two launches: BG1 / BG2 work lists).  The timed step is the
-    decode; the rate recovery of the 12 groups is timed beside it (per-kernel split)."""
+    GPU chain (encode -> rate match -> BPSK+AWGN), OMS beta=0.5, L=8.  The timed step is the
+    receive side: the 12 groups' rate recovery in ONE launch (ldpc5g_sch_raterecover_multi_plan,
+    per-group geometry uploaded once) + the mixed-Zc decode (ldpc5g_decode_ms_mixed_plan, plan built once).  The decode's
+    lane-op roofline is reported twice: on the algorithmic count (all rows x each codeblock's
+    iterations) and on the work the kernel executes (live rows only — a row whose extension column
+    was never transmitted is skipped — x the iterations of the slowest codeblock of each workgroup,
+    which every codeblock packed into that workgroup runs)."""
     import numpy as np
     from python_5gtoolbox_amd.ldpc_info import code_dims
     from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
-    from python_5gtoolbox_amd.sch import cfg_from_codeblocks, sch_ratematch_batch, \
-        sch_raterecover_batch
+    from python_5gtoolbox_amd.sch import SchRaterecoverPlan, cfg_from_codeblocks, sch_ratematch_batch
     rng = np.random.default_rng(404 + rank)
     g = torch.Generator(device=dev)
     g.manual_seed(404 + rank)
     n_per, snr = 341, 1.0
-    groups, info_bits, rr, rr_bytes, edges = [], 0, [], 0, 0
+    cfgs, llrs, info_bits, rr_bytes, meta = [], [], 0, 0, []
     for Zc in (12, 40, 72, 176, 208, 384):
         for bg in (1, 2):
             K, N, _ = code_dims(bg, Zc)
@@ -373,39 +376,88 @@ def bench_config4(torch, dist, world, dev, rank, steps):
             gs = sch_ratematch_batch(ck, cfg, 1)
             sigma = 10 ** (-snr / 20)
             y = (1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g)
-            llr = (2 * y / sigma ** 2).contiguous()
-            dn = sch_raterecover_batch(llr, cfg, dn_dtype=torch.float32).clone()
-            rr.append((llr, cfg))
+            llrs.append((2 * y / sigma ** 2).reshape(-1))
+            cfgs.append(cfg)
             rr_bytes += n_per * (4 * E + 4 * N)   # LLRs in, rate-recovered row out (float32)
-            edges += n_per * (316 if bg == 1 else 197) * Zc
-            groups.append((bg, Zc, dn))
+            meta.append((bg, Zc, K, N))
             info_bits += n_per * K
-    mb = MixedBatch(groups)
+    rrp = SchRaterecoverPlan(cfgs, dev)   # geometry validated and uploaded once
+    lay = rrp.lay
+    llr = torch.zeros((len(cfgs), lay["max_E"]), dtype=torch.float32, device=dev)
+    for t_, x in enumerate(llrs):
+        llr[t_, :x.numel()] = x
+    del llrs
+    dn = rrp(llr, torch.empty((lay["dn"],), dtype=torch.float32, device=dev))
+    groups = [(bg, Zc, dn[r[2]:r[2] + r[1] * N].view(r[1], N)) for (bg, Zc, K, N), r in zip(meta, lay["rows"])]
+    mb = MixedBatch(groups, flat=dn)
     B = mb.B
-    # rate-recovered rows: untransmitted parity columns are +0.0 (LDPC5G_RATE_MATCHED)
-    wall, ev = timed(torch, dist, world, lambda: mb.decode(8, 1.0, 0.5, "layered", True), steps, 2)
+
+    def step():   # rate recovery (one launch) + decode (<= 3 launches), all on the GPU
+        rrp(llr, dn)
+        mb.decode(8, 1.0, 0.5, "layered", True)
+    wall, ev = timed(torch, dist, world, step, steps, 2)
     _, st, it = mb.decode(8, 1.0, 0.5, "layered", True)
-    mean_it = it.float().mean().item()
-    rr_ms = ev_ms(torch, lambda: [sch_raterecover_batch(x, c, dn_dtype=torch.float32)
-                                  for x, c in rr])
+    rr_ms = ev_ms(torch, lambda: rrp(llr, dn))
+    dec_ms = ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, "layered", True))
+    # work accounting on the host: the plan's workgroups (per (bgn, Zc) group: a partial workgroup
+    # of n % G codeblocks first, then full ones of G = floor(768 / Zc) — ldpc5g_capi.hip build_plan)
+    its = it.cpu().numpy().astype(np.int64)
+    dnh = dn.cpu().numpy()
+    alg_edges = exe_edges = wg_iters = 0
+    cb0 = 0
+    for (bg, Zc, K, N), r in zip(meta, lay["rows"]):
+        n = r[1]
+        Gw = 768 // Zc
+        rows_cb = dnh[r[2]:r[2] + n * N].reshape(n, N)
+        # extension column c of the transmitted row layout: columns 2..(N/Zc+1) of the full graph;
+        # ext row i (>= 4) <-> full column KB + i <-> transmitted column KB + i - 2
+        kb = 22 if bg == 1 else 10
+        mb_rows = 46 if bg == 1 else 42
+        live_col = np.abs(rows_cb.reshape(n, N // Zc, Zc)).max(axis=2) != 0   # (n, N/Zc)
+        row_deg = _ROW_DEG[bg]
+        starts = [0] + list(range(n % Gw, n, Gw)) if n % Gw else list(range(0, n, Gw))
+        bounds = starts + [n]
+        for w0, w1 in zip(bounds[:-1], bounds[1:]):
+            if w1 <= w0:
+                continue
+            live = np.ones(mb_rows, bool)
+            lc = live_col[w0:w1].any(axis=0)
+            for i in range(4, mb_rows):
+                live[i] = lc[kb + i - 2]
+            e_live = int(sum(row_deg[i] for i in range(mb_rows) if live[i]))
+            exe_edges += int(its[cb0 + w0:cb0 + w1].max()) * (w1 - w0) * e_live * Zc
+            wg_iters += int(its[cb0 + w0:cb0 + w1].max()) * (w1 - w0)
+        alg_edges += int(its[cb0:cb0 + n].sum()) * sum(row_deg) * Zc
+        cb0 += n
+    mean_it = float(its.mean())
+    dec_alg = valu_line(alg_edges, dec_ms)
+    dec_exe = valu_line(exe_edges, dec_ms)
     return {"workload": "BASELINE config 4: 12 (Zc, BG) groups x 341 CBs, random (Qm, rv, E), "
-                        "GPU rate match/recover, snr 1 dB, layered OMS beta=0.5 L=8, "
-                        "LDPC5G_RATE_MATCHED",
+                        "GPU rate match, snr 1 dB, timed step = rate recovery (one launch) + "
+                        "layered OMS beta=0.5 L=8 decode (LDPC5G_RATE_MATCHED)",
             "codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
             "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
-            "ms_per_call": round(wall / steps * 1e3, 4),
+            "ms_per_step": round(wall / steps * 1e3, 4),
             "mean_iterations": round(mean_it, 3),
             "converged_frac": round(st.float().mean().item(), 4),
             "kernels": {
-                "decode": {**valu_line(edges * mean_it, ev / steps * 1e3),
-                           "note": "edge-updates of the full graphs x mean iterations; rows whose "
-                                   "extension column was never transmitted are skipped by the "
-                                   "kernel (LDPC5G_RATE_MATCHED), so this counts more work than "
-                                   "it does"},
+                "decode": {**dec_alg, "frac_executed": dec_exe["frac"],
+                           "achieved_executed": dec_exe["achieved"], "edge_updates_executed": exe_edges,
+                           "iterations_run_per_codeblock": round(wg_iters / max(B, 1), 3),
+                           "note": "frac: 13 lane-ops x (every row's edges x each codeblock's "
+                                   "iterations); frac_executed: the same over the work the kernel "
+                                   "runs — live rows only x the slowest codeblock's iterations of "
+                                   "each workgroup, for every codeblock packed in it"},
                 "raterecover": {**hbm_line(rr_bytes, rr_ms),
-                                "note": "the 12 groups' sch_raterecover_batch calls (float32 in, "
-                                        "float32 rows out: 4E + 4N bytes per codeblock); not in "
-                                        "the timed step"}}}
+                                "note": "all 12 groups in ONE launch (float32 in, float32 rows out: "
+                                        "4E + 4N bytes per codeblock), inside the timed step"}}}
+
+
+# base-graph row degrees (TS 38.212 Tables 5.3.2-2/-3: edges per base row)
+_ROW_DEG = {1: [19, 19, 19, 19, 3, 8, 9, 7, 10, 9, 7, 8, 7, 6, 7, 7, 6, 6, 6, 6, 6, 6, 5, 5, 6, 5, 5, 4, 5,
+                5, 5, 5, 5, 5, 5, 5, 5, 4, 5, 5, 4, 5, 4, 5, 5, 4],
+            2: [8, 10, 8, 10, 4, 6, 6, 6, 4, 5, 5, 5, 4, 5, 5, 4, 5, 5, 4, 4, 4, 4, 3, 4, 4, 3, 5, 3, 4,
+                3, 5, 3, 4, 4, 4, 4, 4, 3, 4, 4, 4, 4]}
 
 
 def bench_config5(torch, dist, world, dev, rank, steps, T=32):

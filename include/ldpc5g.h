@@ -275,6 +275,20 @@ int ldpc5g_sch_multi_sizes(const ldpc5g_sch_cfg_t* cfgs, int32_t T, int64_t* siz
 int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t ldg,
                             const ldpc5g_sch_cfg_t* cfgs, int32_t T, int8_t* ck, int8_t* dn,
                             uint32_t* tb_crc, void* stream);
+/* rate recovery alone (raterecover_ldpc, py5gphy/ldpc/nr_ldpc_raterecover.py:6-65, + HARQ) of every
+ * codeblock of the T transport blocks in ONE launch, into the flat llr_dn rows (N_t per codeblock,
+ * TB after TB): the input of a mixed-Zc decode (ldpc5g_decode_ms_mixed_plan). */
+int ldpc5g_sch_raterecover_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
+                                 const ldpc5g_sch_cfg_t* cfgs, int32_t T, const void* harq_in,
+                                 void* llr_dn, int32_t dn_dtype, void* stream);
+/* The same with the geometry built once: ldpc5g_sch_multi_plan writes the plan's host bytes (returns
+ * the size needed; call with plan = NULL first), the caller copies them to device memory once, and
+ * every ldpc5g_sch_raterecover_multi_plan(plan_dev, plan_host, ...) only launches (no host-side
+ * validation, allocation or copy per call; asynchronous on `stream`). */
+int64_t ldpc5g_sch_multi_plan(const ldpc5g_sch_cfg_t* cfgs, int32_t T, void* plan, int64_t plan_bytes);
+int ldpc5g_sch_raterecover_multi_plan(const void* plan_dev, const void* plan_host, const void* llr,
+                                      int32_t llr_dtype, int64_t ldg, const void* harq_in, void* llr_dn,
+                                      int32_t dn_dtype, void* stream);
 /* decode: rate recovery (+ HARQ, harq_in laid out like llr_dn) -> mixed-Zc min-sum decode of all
  * codeblocks (ldpc5g_decode_ms_mixed) -> TB reassembly + CRCs.  Asynchronous on `stream`. */
 int ldpc5g_sch_decode_multi(const void* llr, int32_t llr_dtype, int64_t ldg,

@@ -87,6 +87,13 @@ SIGNATURES = {
     "ldpc5g_sch_encode_multi": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_int64,
                                            _c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_void_p,
                                            _c.c_void_p, _c.c_void_p]),
+    "ldpc5g_sch_raterecover_multi": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p,
+                                                _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                                _c.c_void_p]),
+    "ldpc5g_sch_multi_plan": (_c.c_int64, [_c.c_void_p, _c.c_int32, _c.c_void_p, _c.c_int64]),
+    "ldpc5g_sch_raterecover_multi_plan": (_c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                                     _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_int32,
+                                                     _c.c_void_p]),
     "ldpc5g_sch_decode_multi": (_c.c_int, [_c.c_void_p, _c.c_int32, _c.c_int64, _c.c_void_p,
                                            _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_int32,
                                            _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32,

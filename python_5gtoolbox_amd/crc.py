@@ -39,8 +39,44 @@ def _table(poly):
     return _TAB[poly]
 
 
+_POS = {}
+
+
+def _pos_table(poly, n):
+    """x^(n-1-i+L) mod G(x) for every bit position i of an n-bit message (uint32), cached per
+    (poly, n): the remainder of a message is the XOR of the entries of its 1 bits (CRC is linear),
+    one vectorised reduction instead of a per-byte Python loop (~0.4 ms per 8448-bit codeblock)."""
+    key = (poly, n)
+    t = _POS.get(key)
+    if t is None:
+        p = _POLY[poly]
+        L = len(p)
+        g = int("".join(map(str, p)), 2) & ((1 << L) - 1)   # x^L term implied
+        mask = (1 << L) - 1
+        top = 1 << (L - 1)
+        t = np.zeros(n, np.uint32)
+        r = g   # x^L mod G
+        for i in range(n - 1, -1, -1):
+            t[i] = r
+            r = ((r << 1) & mask) ^ (g if r & top else 0)
+        if len(_POS) > 256:
+            _POS.clear()
+        _POS[key] = t
+    return t
+
+
 def _remainder(bits, poly):
     """M(x) * x^L mod G(x) of the MSB-first bit sequence (crc.py:28-33 long division)."""
+    bits = np.asarray(bits)
+    if bits.size >= 64:
+        t = _pos_table(poly, bits.size)
+        sel = t & (-(bits.astype(np.int32) & 1)).view(np.uint32)   # entries of the 1 bits
+        return int(np.bitwise_xor.reduce(sel)), len(_POLY[poly])
+    return _remainder_bytes(bits, poly)
+
+
+def _remainder_bytes(bits, poly):
+    """The same by byte-table long division (short messages)."""
     L, tab = _table(poly)
     n = bits.size
     head = n % 8
@@ -89,7 +125,8 @@ def nr_crc_encode(blk, poly, mask=0):
 
 def nr_crc_decode(blkandcrc, poly, mask=0):
     x = np.asarray(blkandcrc)
-    assert (not np.any(np.nonzero(x < 0))) and (not np.any(np.nonzero(x > 1)))
+    if x.size and (x.min() < 0 or x.max() > 1):   # the reference's own test, verbatim semantics (crc.py:53-54)
+        assert (not np.any(np.nonzero(x < 0))) and (not np.any(np.nonzero(x > 1)))
     x = x.astype("i1")
     poly = poly.upper()
     assert poly in _POLY

@@ -177,6 +177,30 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
     return need;
 }
 
+// A second stream per (thread, device) for the BG2 half of a mixed plan: the BG1 and BG2 launches
+// then share the GPU instead of running one after the other (each alone leaves a partly idle last
+// round of workgroups).  Ordered against the caller's stream by two events; created once, never
+// destroyed (like the staging buffers).
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+thread_local SideStream t_side[64];
+
+int side_stream(SideStream** out) {
+    int dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (dev < 0 || dev >= 64) return fail(LDPC5G_ESIZE, "device ordinal %d >= 64", dev);
+    SideStream& x = t_side[dev];
+    if (!x.s) {
+        if (int rc = check_hip(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking), "hipStreamCreate(side)")) return rc;
+        if (int rc = check_hip(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming), "hipEventCreate(fork)")) return rc;
+        if (int rc = check_hip(hipEventCreateWithFlags(&x.join, hipEventDisableTiming), "hipEventCreate(join)")) return rc;
+    }
+    *out = &x;
+    return LDPC5G_OK;
+}
+
 // launches of a plan (host copy `h` for the counts, device copy `dev` for the kernels)
 int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr_base, int llr_dtype,
                 int8_t* ck_base, uint8_t* status, int32_t* iters, int L, double alpha, double beta,
@@ -193,16 +217,28 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     // 1.17 ms split off)
     constexpr int kZcSplitMin = 512;
     const int nz = (lay || llr_dtype == LDPC5G_F64) && h.nz1 >= kZcSplitMin ? std::min(h.nz1, h.nw1) : 0;
+    // BG2 on the side stream when both base graphs are present (forked from / joined into st)
+    SideStream* side = nullptr;
+    if (h.nw2 > 0 && h.nw1 > 0) {
+        if (int rc = side_stream(&side)) return rc;
+        if (int rc = check_hip(hipEventRecord(side->fork, st), "hipEventRecord(fork)")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "hipStreamWaitEvent(fork)")) return rc;
+    }
     for (int g = 0; g < 2; ++g) {
         const int nwg = g == 0 ? h.nw1 - nz : h.nw2;
+        hipStream_t sg = g == 1 && side ? side->s : st;
         if (nwg > 0)
             if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
-                                          g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, st))
+                                          g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, sg))
                 return rc;
         if (g == 0 && nz > 0)
             if (int rc = launch_dec_mixed(1, llr_dtype, lay, llr_base, ck_base, status, iters, nz,
                                           w1 + (h.nw1 - nz), r, L, alpha, beta, pc, dead, st, true))
                 return rc;
+    }
+    if (side) {
+        if (int rc = check_hip(hipEventRecord(side->join, side->s), "hipEventRecord(join)")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(st, side->join, 0), "hipStreamWaitEvent(join)")) return rc;
     }
     return LDPC5G_OK;
 }

@@ -394,6 +394,8 @@ __global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict
 
 // -------------------------------------------------------------------------------- receive
 constexpr int kRrNT = 512;
+// the E LLRs of a codeblock are staged in LDS up to this size (4 x 512-thread workgroups per CU)
+constexpr int kRrStageBytes = 40 * 1024;
 
 template <typename Tin>
 __device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double)p[i]; }
@@ -406,9 +408,10 @@ __device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double
 // STAGE: the codeblock's E input LLRs are first copied into LDS in de-interleaved order
 // (lds[q*EQ + r] = llr[r*Qm + q], i.e. lds[k] is the k-th bit of the interleaver's column read-out),
 // in the same pass as the max|LLR| reduction: the input is read once, coalesced, and the gather
-// below reads LDS at consecutive k instead of global memory at stride Qm.  Without STAGE (E too
-// large for LDS) the gather reads global memory.  Outputs: 4 consecutive positions per thread,
-// stored as 16-B pieces when the row is 16-B aligned.
+// below reads LDS at consecutive k instead of global memory at stride Qm.  A row whose E is too
+// large for the stage gathers from global memory (decided per row).  Rows without repetition
+// (E <= size, the common case) take neither: see the k-major pass below.  Outputs of the gather:
+// 4 consecutive positions per thread, stored as 16-B pieces when the row is 16-B aligned.
 template <typename Tin, typename Tout, bool STAGE>
 __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restrict__ llr, int64_t ldg,
                                                             SchDev s0, const SchGeo* __restrict__ gv,
@@ -423,8 +426,33 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     const int t = rg.t, c = rg.c;
     const int E = cb_E(s, c), EQ = E / s.Qm;
     const Tin* fe = llr + (int64_t)t * ldg + cb_goff(s, c);
+    const int64_t row = rg.dn_row;
+    Tout* orow = out + row;
+    auto combine = [&](double v, int p) -> double {   // HARQ (nr_dlsch_decode.py:73-88)
+        if (harq) {
+            const double h = (double)harq[row + p];
+            v = (v == 0.0 || h == 0.0) ? v + h : (v + h) / 2.0;
+        }
+        return v;
+    };
     double m = 0.0;
-    if constexpr (STAGE) {
+    if (E <= s.size) {
+        // no repetition: every visited position holds exactly one LLR, (0.0 + x) / 1.  Bit k of
+        // the column read-out (k = q*EQ + r) is LLR r*Qm + q and lands at the position of rank k in
+        // the circular order from k0.  A thread per r reads its Qm consecutive LLRs (coalesced) and
+        // writes them plane by plane: consecutive r -> consecutive positions (coalesced too).
+        for (int r = threadIdx.x; r < EQ; r += kRrNT) {
+            const Tin* src = fe + (int64_t)r * s.Qm;
+            for (int q = 0; q < s.Qm; ++q) {
+                const double x = (double)src[q];
+                m = fmax(m, fabs(x));
+                int pp = q * EQ + r + s.start;   // rank + start, in the filler-free index space
+                if (pp >= s.size) pp -= s.size;
+                const int p = pp < s.f0 ? pp : pp + s.Fin;
+                orow[p] = (Tout)combine(0.0 + x, p);
+            }
+        }
+    } else if (STAGE && E * (int)sizeof(Tin) <= kRrStageBytes) {   // per row: this row fits
         for (int r = threadIdx.x; r < EQ; r += kRrNT) {
             const Tin* src = fe + (int64_t)r * s.Qm;
             for (int q = 0; q < s.Qm; ++q) {
@@ -444,8 +472,27 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
 #pragma unroll
     for (int w = 1; w < kRrNT / 64; ++w) m = fmax(m, red[w]);
     const double mx = m * 10.0;
-    const int64_t row = rg.dn_row;
     const int qE = E / s.size, rE = E - qE * s.size;   // visits of rank rr: qE + (rr < rE)
+    const bool stg = STAGE && E * (int)sizeof(Tin) <= kRrStageBytes;
+    if (E <= s.size) {
+        // the positions the read-out did not reach: fillers 10 * max|LLR|, unvisited ranks and the
+        // tail past Ncb 0 (+ HARQ); disjoint from the positions written above
+        for (int p = threadIdx.x; p < s.N; p += kRrNT) {
+            double v;
+            if (p >= s.f0 && p < s.f0 + s.F) {
+                v = mx;
+            } else if (p < s.Ncb) {
+                int rr = (p < s.f0 ? p : p - s.Fin) - s.start;
+                if (rr < 0) rr += s.size;
+                if (rr < E) continue;
+                v = 0.0;
+            } else {
+                v = 0.0;
+            }
+            orow[p] = (Tout)combine(v, p);
+        }
+        return;
+    }
     auto value = [&](int p) -> double {
         double v = 0.0;
         if (p >= s.f0 && p < s.f0 + s.F) {
@@ -458,19 +505,14 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
                 double acc = 0.0;
                 for (int j = 0; j < cnt; ++j) {
                     const int k = rr + j * s.size;
-                    if constexpr (STAGE) acc += (double)lk[k];
+                    if (STAGE && stg) acc += (double)lk[k];
                     else acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
                 }
                 v = cnt == 1 ? acc : acc / (double)cnt;   // x / 1.0 == x: skip the f64 divide
             }
         }
-        if (harq) {
-            const double h = (double)harq[row + p];
-            v = (v == 0.0 || h == 0.0) ? v + h : (v + h) / 2.0;
-        }
-        return v;
+        return combine(v, p);
     };
-    Tout* orow = out + row;
     const bool vec = ((uintptr_t)orow & 15) == 0;
     for (int p0 = 4 * (int)threadIdx.x; p0 < s.N; p0 += 4 * kRrNT) {
         Tout v[4];
@@ -567,19 +609,15 @@ int64_t sch_total_E(const SchDev& s) {
     return (int64_t)s.c_switch * s.E_lo + (int64_t)(s.C - s.c_switch) * s.E_hi;
 }
 
-// the E LLRs of a codeblock are staged in LDS up to this size (4 x 512-thread workgroups per CU)
-constexpr int kRrStageBytes = 40 * 1024;
 
 template <typename Tin, typename Tout>
 void raterecover_go(dim3 grid, const void* llr, int64_t ldg, const SchDev& s, const SchGeo* gv,
                     const RowRef* rm, const void* harq_in, void* llr_dn, int max_cb_E, hipStream_t st) {
-    const size_t lds = (size_t)max_cb_E * sizeof(Tin);
-    if (lds <= (size_t)kRrStageBytes)
-        hipLaunchKernelGGL((raterecover_kernel<Tin, Tout, true>), grid, dim3(kRrNT), lds, st, (const Tin*)llr, ldg, s,
-                           gv, rm, (const Tout*)harq_in, (Tout*)llr_dn);
-    else
-        hipLaunchKernelGGL((raterecover_kernel<Tin, Tout, false>), grid, dim3(kRrNT), 0, st, (const Tin*)llr, ldg, s,
-                           gv, rm, (const Tout*)harq_in, (Tout*)llr_dn);
+    // rows whose E fits the stage use it (decided per row in the kernel): the launch's LDS is the
+    // stage size capped by its largest codeblock
+    const size_t lds = std::min((size_t)max_cb_E * sizeof(Tin), (size_t)kRrStageBytes);
+    hipLaunchKernelGGL((raterecover_kernel<Tin, Tout, true>), grid, dim3(kRrNT), lds, st, (const Tin*)llr, ldg, s,
+                       gv, rm, (const Tout*)harq_in, (Tout*)llr_dn);
 }
 
 // max_cb_E: the largest per-codeblock E of the launch (sizes the LDS stage)
@@ -870,6 +908,80 @@ int ldpc5g_sch_encode_multi(const int8_t* trblk, int64_t lda, int8_t* g, int64_t
         hipLaunchKernelGGL(ratematch_kernel, dim3(rows, (m.max_EQ + 255) / 256), dim3(256), 0, st, dn, s0,
                            m.dgeo(), m.drows(), g, ldg);
     if (int rc = check_hip(hipGetLastError(), "ratematch launch")) return rc;
+    return m.release();
+}
+
+}  // extern "C"
+
+namespace ldpc5g_impl {
+namespace {
+// Reusable multi-configuration rate-recovery plan (host bytes, copied verbatim to the device):
+//   SchPlanHdr | SchGeo[T] | RowRef[rows]
+struct SchPlanHdr {
+    int32_t magic, T, rows, max_cb_E;
+    int64_t max_E, dn_elems;
+};
+constexpr int32_t kSchPlanMagic = 0x4c505253;   // "SRPL"
+}  // namespace
+}  // namespace ldpc5g_impl
+
+extern "C" {
+
+int64_t ldpc5g_sch_multi_plan(const ldpc5g_sch_cfg_t* cfgs, int32_t T, void* plan, int64_t plan_bytes) {
+    clear_error();
+    SchMulti m;
+    if (int rc = m.build(cfgs, T)) return rc;
+    const int64_t gb = (int64_t)m.geo.size() * (int64_t)sizeof(SchGeo), rb = (int64_t)m.rows.size() * (int64_t)sizeof(RowRef);
+    const int64_t need = (int64_t)sizeof(SchPlanHdr) + gb + rb;
+    if (!plan || plan_bytes < need) return need;
+    SchPlanHdr h{kSchPlanMagic, T, (int32_t)m.rows.size(), 0, m.max_E, m.dn_elems};
+    for (const SchGeo& g : m.geo) h.max_cb_E = std::max(h.max_cb_E, std::max(g.s.E_lo, g.s.E_hi));
+    unsigned char* p = (unsigned char*)plan;
+    memcpy(p, &h, sizeof h);
+    memcpy(p + sizeof h, m.geo.data(), (size_t)gb);
+    memcpy(p + sizeof h + gb, m.rows.data(), (size_t)rb);
+    return need;
+}
+
+int ldpc5g_sch_raterecover_multi_plan(const void* plan_dev, const void* plan_host, const void* llr,
+                                      int32_t llr_dtype, int64_t ldg, const void* harq_in, void* llr_dn,
+                                      int32_t dn_dtype, void* stream) {
+    clear_error();
+    if (!plan_dev || !plan_host) return fail(LDPC5G_ESIZE, "null plan");
+    SchPlanHdr h;
+    memcpy(&h, plan_host, sizeof h);
+    if (h.magic != kSchPlanMagic) return fail(LDPC5G_ESIZE, "not a rate-recovery plan (ldpc5g_sch_multi_plan)");
+    if ((llr_dtype != LDPC5G_F32 && llr_dtype != LDPC5G_F64) || (dn_dtype != LDPC5G_F32 && dn_dtype != LDPC5G_F64))
+        return fail(LDPC5G_ESIZE, "bad dtype");
+    if (h.T > 1 && ldg < h.max_E) return fail(LDPC5G_ESIZE, "bad stride ldg=%lld (max E %lld)", (long long)ldg, (long long)h.max_E);
+    if (h.rows == 0) return LDPC5G_OK;
+    if (!llr || !llr_dn) return fail(LDPC5G_ESIZE, "null buffer");
+    const SchGeo* g = (const SchGeo*)((const unsigned char*)plan_dev + sizeof(SchPlanHdr));
+    const RowRef* r = (const RowRef*)(g + h.T);
+    const SchDev s0{};
+    return launch_raterecover(dim3((unsigned)h.rows), llr, llr_dtype, ldg, s0, g, r, harq_in, llr_dn, dn_dtype,
+                              h.max_cb_E, (hipStream_t)stream);
+}
+
+int ldpc5g_sch_raterecover_multi(const void* llr, int32_t llr_dtype, int64_t ldg,
+                                 const ldpc5g_sch_cfg_t* cfgs, int32_t T, const void* harq_in,
+                                 void* llr_dn, int32_t dn_dtype, void* stream) {
+    clear_error();
+    SchMulti m;
+    if (int rc = m.build(cfgs, T)) return rc;
+    if ((llr_dtype != LDPC5G_F32 && llr_dtype != LDPC5G_F64) || (dn_dtype != LDPC5G_F32 && dn_dtype != LDPC5G_F64))
+        return fail(LDPC5G_ESIZE, "bad dtype");
+    if (T > 1 && ldg < m.max_E) return fail(LDPC5G_ESIZE, "bad stride ldg=%lld (max E %lld)", (long long)ldg, (long long)m.max_E);
+    if (T == 0) return LDPC5G_OK;
+    if (!llr || !llr_dn) return fail(LDPC5G_ESIZE, "null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = m.upload(st)) return rc;
+    int max_cb_E = 0;
+    for (const SchGeo& g : m.geo) max_cb_E = std::max(max_cb_E, std::max(g.s.E_lo, g.s.E_hi));
+    const SchDev s0{};
+    if (int rc = launch_raterecover(dim3((unsigned)m.rows.size()), llr, llr_dtype, ldg, s0, m.dgeo(), m.drows(),
+                                    harq_in, llr_dn, dn_dtype, max_cb_E, st))
+        return rc;
     return m.release();
 }
 

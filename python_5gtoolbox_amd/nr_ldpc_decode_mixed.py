@@ -50,9 +50,11 @@ class MixedBatch:
     rows of several (bgn, Zc) groups concatenated in one flat float32 LLR buffer, with the
     descriptor array (ldpc5g_cb_desc_t) built once.
 
-    groups: list of (bgn, Zc, llr (n, N) float32 device tensor)."""
+    groups: list of (bgn, Zc, llr (n, N) float32 device tensor).  flat: an existing flat float32
+    buffer holding exactly those rows back to back in group order (e.g. sch_raterecover_multi's
+    output, whose row groups are views of it): used in place, nothing is copied."""
 
-    def __init__(self, groups):
+    def __init__(self, groups, flat=None):
         t = _lib.require_gpu()
         B = sum(g[2].shape[0] for g in groups)
         self.desc = (_lib.CbDesc * max(B, 1))()
@@ -71,7 +73,11 @@ class MixedBatch:
                 k += 1
             parts.append(llr.reshape(-1))
         dev = groups[0][2].device
-        self.llr = t.cat(parts).contiguous()
+        if flat is not None:
+            assert flat.dtype == t.float32 and flat.is_contiguous() and flat.numel() >= lo
+            self.llr = flat
+        else:
+            self.llr = t.cat(parts).contiguous()
         self.ck = t.empty(max(co, 1), dtype=t.int8, device=dev)
         self.status = t.empty(max(B, 1), dtype=t.uint8, device=dev)
         self.iters = t.empty(max(B, 1), dtype=t.int32, device=dev)

@@ -7,31 +7,45 @@ call surface); the batched GPU rate recovery + HARQ combining is `raterecover_ke
 import numpy as np
 
 
+_ORDER = {}
+
+
+def _visit_order(Ncb, k0, filler):
+    """The non-filler positions of the circular buffer in the order the bit selection visits them
+    from k0 (one lap), cached per geometry."""
+    key = (Ncb, k0, filler.tobytes())
+    o = _ORDER.get(key)
+    if o is None:
+        isfill = np.zeros(Ncb, bool)
+        isfill[filler[(filler >= 0) & (filler < Ncb)]] = True
+        cyc = (k0 + np.arange(Ncb)) % Ncb
+        o = cyc[~isfill[cyc]]
+        if len(_ORDER) > 256:
+            _ORDER.clear()
+        _ORDER[key] = o
+    return o
+
+
 def raterecover_ldpc(LLr_fe, Ncb, N, k0, Qm, Zc, K_apo, K):
     LLr_fe = np.asarray(LLr_fe, np.float64)
     E = LLr_fe.size
-    LLr_ek = LLr_fe.reshape(E // Qm, Qm).T.reshape(E)
+    LLr_ek = LLr_fe.reshape(E // Qm, Qm).T.reshape(E)   # bit de-interleaving (:24-27)
     max_LLR = np.max(np.abs(LLr_fe)) * 10
     filler = np.arange(K_apo, K) - 2 * Zc
-    isfill = np.zeros(Ncb, bool)
-    isfill[filler[(filler >= 0) & (filler < Ncb)]] = True
-    # visit order of the circular buffer from k0; non-filler visits consume LLRs in order
-    size = Ncb - filler.size
+    # LLR j lands in lap j // size at the (j % size)-th non-filler position visited from k0: the
+    # reference's tmp_buf[rep, pos] (:34-52); its column sums (rows in order, zeros where a lap did
+    # not reach) are reproduced by the same axis-0 sum over the laps
+    order = _visit_order(Ncb, k0, filler)
+    size = order.size
     rep_num = int(np.ceil(E / size))
-    cyc = (k0 + np.arange(Ncb)) % Ncb
-    keep = ~isfill[cyc]
-    # number of whole/partial passes needed to consume E non-filler positions
-    npass = rep_num + 1
-    visit = np.tile(cyc, npass)
-    take = np.tile(keep, npass)
-    last = np.nonzero(take)[0][E - 1]          # index of the E-th consumed position
-    visit, take = visit[:last + 1], take[:last + 1]
-    rep = np.arange(visit.size) // Ncb         # pass index (row of the reference's tmp_buf)
-    tmp = np.zeros((rep_num, Ncb))
-    tmp[rep[take], visit[take]] = LLr_ek
-    cnt = np.bincount(visit, minlength=Ncb).astype(np.float64)
+    tmp = np.zeros(rep_num * size)
+    tmp[:E] = LLr_ek
+    s = np.sum(tmp.reshape(rep_num, size), axis=0)
+    # visits per position (filler positions excluded: they are overwritten below); 0 -> 10000 (:57)
+    cnt = np.full(size, float(rep_num))
+    cnt[E - (rep_num - 1) * size:] -= 1.0
     cnt[cnt == 0] = 10000
     LLr_dn = np.zeros(N)
-    LLr_dn[0:Ncb] = np.sum(tmp, axis=0) / cnt
+    LLr_dn[order] = s / cnt
     LLr_dn[filler] = max_LLR
     return LLr_dn

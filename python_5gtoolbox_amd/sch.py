@@ -278,6 +278,59 @@ def sch_encode_multi(trblk, cfgs):
     return g
 
 
+def sch_raterecover_multi(llr, cfgs, harq_in=None, dn_dtype=None, out=None, lay=None):
+    """Rate recovery (raterecover_ldpc, py5gphy/ldpc/nr_ldpc_raterecover.py:6-65) of T transport
+    blocks with per-TB configurations in ONE launch (ldpc5g_sch_raterecover_multi).
+    llr: (T, >= max E_total) float32/64 device tensor.  Returns the flat llr_dn (codeblock rows of
+    N_t, TB after TB; multi_layout(cfgs)["rows"] locates them) of dn_dtype (default llr's)."""
+    t = _lib.require_gpu()
+    T = len(cfgs)
+    lay = lay or multi_layout(cfgs)
+    assert llr.dim() == 2 and llr.shape[0] == T and llr.stride(1) == 1 and llr.shape[1] >= lay["max_E"]
+    dn_dtype = dn_dtype or llr.dtype
+    if out is None:
+        out = t.empty((max(lay["dn"], 1),), dtype=dn_dtype, device=llr.device)
+    assert out.dtype == dn_dtype and out.numel() >= lay["dn"] and out.is_contiguous()
+    if harq_in is not None:
+        assert harq_in.dtype == dn_dtype and harq_in.numel() >= lay["dn"] and harq_in.is_contiguous()
+    with t.cuda.device(llr.device):
+        _lib.check(_lib.lib().ldpc5g_sch_raterecover_multi(
+            _lib.ptr(llr), _dtype_id(t, llr.dtype), llr.stride(0), lay["arr"], T,
+            _lib.ptr(harq_in) if harq_in is not None else None, _lib.ptr(out), _dtype_id(t, dn_dtype),
+            _lib.stream_ptr(llr.device)))
+    return out
+
+
+class SchRaterecoverPlan:
+    """sch_raterecover_multi for repeated use: the per-TB geometry is validated and copied to the
+    device once (ldpc5g_sch_multi_plan); each call only launches the kernel
+    (ldpc5g_sch_raterecover_multi_plan), asynchronously on the current stream."""
+
+    def __init__(self, cfgs, device):
+        t = _lib.require_gpu()
+        lib = _lib.lib()
+        self.lay = multi_layout(cfgs)
+        self.T = len(cfgs)
+        n = lib.ldpc5g_sch_multi_plan(self.lay["arr"], self.T, None, 0)
+        _lib.check(int(min(n, 0)))
+        self.host = t.empty((max(n, 1),), dtype=t.uint8, pin_memory=True)
+        _lib.check(int(min(lib.ldpc5g_sch_multi_plan(self.lay["arr"], self.T, _lib.ptr(self.host), n), 0)))
+        self.dev = self.host.to(device, non_blocking=True)
+
+    def __call__(self, llr, out, harq_in=None):
+        t = _lib.torch()
+        assert llr.dim() == 2 and llr.shape[0] == self.T and llr.stride(1) == 1
+        assert llr.shape[1] >= self.lay["max_E"] and out.is_contiguous() and out.numel() >= self.lay["dn"]
+        if harq_in is not None:
+            assert harq_in.dtype == out.dtype and harq_in.numel() >= self.lay["dn"] and harq_in.is_contiguous()
+        with t.cuda.device(llr.device):
+            _lib.check(_lib.lib().ldpc5g_sch_raterecover_multi_plan(
+                _lib.ptr(self.dev), _lib.ptr(self.host), _lib.ptr(llr), _dtype_id(t, llr.dtype),
+                llr.stride(0), _lib.ptr(harq_in) if harq_in is not None else None, _lib.ptr(out),
+                _dtype_id(t, out.dtype), _lib.stream_ptr(llr.device)))
+        return out
+
+
 def sch_decode_multi(llr, cfgs, L, alpha=1.0, beta=0.0, schedule="flooding", harq_in=None,
                      dn_dtype=None):
     """DLSCHDecode / ULSCH_decoding of T transport blocks with per-TB configurations in one call

@@ -476,3 +476,39 @@ def test_sch_multi_random_configs_vs_oracle(torch, sch, seed):
         assert np.array_equal(ck[dck:dck + C * nf].reshape(C, nf), rck), t
         rok, blk, _ = O.sch_tb_check(rck, p)
         assert ok[t] == rok and np.array_equal(tbblk[t, :a[0]], blk), t
+
+
+@pytest.mark.parametrize("dt", ["float64", "float32"])
+def test_sch_raterecover_multi_matches_per_config(torch, sch, dt):
+    """ldpc5g_sch_raterecover_multi (every TB's rate recovery in ONE launch, per-TB geometry:
+    the config-4 receive step) == the single-configuration rate recovery run per TB, bit for bit,
+    including a HARQ-combined second call; float64 and float32 outputs.  (The single-config
+    kernel is itself bit-exact vs the reference's raterecover_ldpc goldens.)"""
+    rng = np.random.default_rng(17)
+    specs = [(24000, 4, 700, 1, 0, 60000, 30000), (3000, 2, 300, 1, 1, 10000, 9000),
+             (60000, 8, 900, 2, 2, 60000, 64000), (500, 6, 120, 1, 3, 0, 4200)]
+    cfgs = [sch.sch_config(*a) for a in specs]
+    # config-4 style codeblock groups too (ULSCH_encoding_ratematch geometry, no TB CRC use)
+    for Zc, bg, Qm, rv in ((12, 2, 4, 1), (384, 1, 8, 3), (40, 1, 2, 0)):
+        K = (22 if bg == 1 else 10) * Zc
+        N = (66 if bg == 1 else 50) * Zc
+        E = Qm * int(rng.integers(-(-K // Qm), int(1.6 * N) // Qm + 1))
+        cfgs.append(sch.cfg_from_codeblocks(7, K, K, Zc, bg, Qm, 7 * E, 1, rv))
+    T = len(cfgs)
+    lay = sch.multi_layout(cfgs)
+    tdt = getattr(torch, dt)
+    llr = torch.zeros((T, lay["max_E"]), dtype=tdt, device="cuda")
+    for t, c in enumerate(cfgs):
+        llr[t, :c.E_total] = torch.from_numpy(rng.normal(0, 3, c.E_total)).to(tdt)
+    flat = sch.sch_raterecover_multi(llr, cfgs, lay=lay)
+    flat2 = sch.sch_raterecover_multi(llr, cfgs, harq_in=flat, lay=lay)
+    plan = sch.SchRaterecoverPlan(cfgs, llr.device)   # the reusable-plan form: same bytes
+    viaplan = torch.full_like(flat, float("nan"))
+    assert torch.equal(plan(llr, viaplan), flat)
+    for t, c in enumerate(cfgs):
+        x = llr[t:t + 1, :c.E_total].contiguous()
+        one = sch.sch_raterecover_batch(x, c).clone()
+        _, C, off, N, _, _ = lay["rows"][t]
+        assert torch.equal(flat[off:off + C * N].view(C, N), one), t
+        two = sch.sch_raterecover_batch(x, c, harq_in=one.contiguous())
+        assert torch.equal(flat2[off:off + C * N].view(C, N), two), t
