@@ -139,22 +139,19 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bf_kernel(
 }
 
 // ------------------------------------------------------------------------------------- BP
-// Two phases per iteration, as the min-sum flooding kernel, but per-edge messages (they do not
-// compress) in the caller's scratch msg[cb][e][z] (coalesced over z):
-//   phase A  every row (a runtime loop; the row body instantiated per degree, tanh / atanh inlined
-//            once per edge slot of that degree) reads LQ_old (LDS) and r_old (scratch), forms
-//            q = LQ_old - r_old, t = tanh(q/2) and writes r_new over r_old; the syndrome of LQ_old
-//            comes from the same reads.  The next row's r_old loads are issued before the current
-//            row's arithmetic, so their latency hides behind it.  No barrier between rows.
-//   phase B  a column-owner gather: each core column entry sums the messages of its rows in
-//            ascending row order (Lr.sum(axis=0), :126) straight from the scratch, into a register,
-//            then writes LQ = LLR + sum over LQ_old in LDS.  No barrier between columns.
-// One thread per slot (z, codeblock), 384-thread workgroups holding only the LQ image (80 KB), so
-// two workgroups (two codeblocks of Zc = 384) share a CU and cover each other's barriers.
-constexpr int kBpThreads = 384;
+// Float64 sum-product flooding (nr_ldpc_decode.py:51-143, _BP_process :145-176).  Per-edge
+// messages do not compress, so they live in the caller's scratch (layout below); LQ_old and the
+// row-ascending sums Lr.sum(axis=0) of the core columns live in LDS (2 x 80 KB at Zc = 384, one
+// workgroup per CU).  Every slot (z, codeblock) has TWO lanes, adjacent in the wave: the even and
+// the odd edges of every row.  Rows run in order (a runtime loop; the row body is unrolled over
+// the lane's <= 10 edges, tanh / atanh inlined once per edge slot); a barrier only where a new
+// group of column-disjoint rows starts (BG1: 32 per iteration), so the LDS sums keep the
+// reference's row order; the lane pair combines its partial products, zero counts and syndrome
+// parity with one DPP lane swap (no LDS).  The next row's messages are loaded before the current
+// row's arithmetic.  r05: 19.8 -> 10.7 ms per 1024 BG1 Zc=384 codeblocks (L=8).
+constexpr int kBpThreads = 768;   // two lanes per slot (even / odd edges of every row)
 constexpr double kBpClip = 2.0 * 19.07;   // (:159,161)
 constexpr int kBpMaxDeg = 19;
-constexpr int kBpPrefetch = 10;   // r_old loads issued one row ahead (edges 0..9: every row but rows 0-3 of BG1)
 
 template <int BG>
 constexpr int bp_max_deg() {
@@ -242,170 +239,234 @@ __device__ __forceinline__ double bp_two_atanh(double y, const BpAtanhK& K) {
     return copysign(r, y);
 }
 
+// Consecutive base rows with disjoint core columns (the grouping of ldpc5g_dec_body.h RowGroups):
+// their sums into a column never meet, so a group needs no barrier inside it.
 template <int BG>
-__global__ __launch_bounds__(kBpThreads, 3) void ldpc_bp_kernel(
+struct BpGroups {
+    int n = 0;
+    int start[64] = {};
+    constexpr BpGroups() {
+        using P = BGT<BG>;
+        int g0 = 0;
+        n = 1;
+        for (int i = 1; i < P::MB; ++i) {
+            bool dis = true;
+            for (int a = g0; a < i && dis; ++a)
+                for (int e = P::RS[a]; e < P::RS[a + 1]; ++e)
+                    for (int f = P::RS[i]; f < P::RS[i + 1]; ++f)
+                        if (P::COL[e] == P::COL[f] && P::COL[e] < P::KC) dis = false;
+            if (!dis) start[n++] = i, g0 = i;
+        }
+        start[n] = P::MB;
+    }
+};
+template <int BG>
+constexpr BpGroups<BG> kBpGroups{};
+
+// Message scratch layout: the edges of row i are taken in pairs (k = 2kk, 2kk + 1; a row of odd
+// degree pads its last pair), pair slot P(i, kk) = PS[i] + kk, and a pair's two messages of slot z
+// are adjacent: msg[cb][P][z][2] -- the two lanes of a slot (even / odd edges) touch consecutive
+// 8-B words, so a wave's message loads and stores are 512 contiguous bytes.
+template <int BG>
+struct BpPairs {
+    int ps[64] = {};   // first pair slot of row i
+    int np = 0;        // pair slots per codeblock
+    bool first[64] = {};   // row i starts a group of column-disjoint rows (RowGroups)
+    constexpr BpPairs() {
+        using P = BGT<BG>;
+        for (int i = 0; i < P::MB; ++i) ps[i] = np, np += (P::RS[i + 1] - P::RS[i] + 1) / 2;
+        for (int g = 0; g < kBpGroups<BG>.n; ++g) first[kBpGroups<BG>.start[g]] = true;
+    }
+};
+template <int BG>
+constexpr BpPairs<BG> kBpPairs{};
+__constant__ BpPairs<1> kBpPairsD1 = kBpPairs<1>;   // device copies (runtime row index)
+__constant__ BpPairs<2> kBpPairsD2 = kBpPairs<2>;
+template <int BG>
+__device__ __forceinline__ const BpPairs<BG>& bp_pairs_d() {
+    if constexpr (BG == 1) return kBpPairsD1;
+    else return kBpPairsD2;
+}
+
+// the pair partner's value (lanes 2s <-> 2s+1): DPP quad_perm [1,0,3,2], no LDS
+__device__ __forceinline__ uint32_t pair_swap(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double pair_swap(double x) {
+    const uint32_t lo = pair_swap((uint32_t)__double2loint(x)), hi = pair_swap((uint32_t)__double2hiint(x));
+    return __hiloint2double((int)hi, (int)lo);
+}
+
+template <int BG>
+__global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
     const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, double* __restrict__ msg, int B, int Zc, int zi, int G,
     int64_t ldl, int64_t ldc, int L, int pc) {
     using P = BGT<BG>;
-    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, E = P::E, DM = bp_max_deg<BG>();
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, DM = bp_max_deg<BG>(), KK = (DM + 1) / 2;
+    constexpr int NPAIR = kBpPairs<BG>.np;
     extern __shared__ __align__(16) unsigned char smem[];
-    double* app = (double*)smem;              // [KC][kCS] LQ of the core columns
-    int* flag = (int*)(app + KC * kCS);       // [kCS] per codeblock slot
+    double* app = (double*)smem;              // [KC][kCS] LQ of the core columns (LQ_old in a pass)
+    double* acc = app + KC * kCS;             // [KC][kCS] Lr.sum(axis=0), rows ascending
+    int* flag = (int*)(acc + KC * kCS);       // [kCS] per codeblock slot
     const int t = threadIdx.x;
-    const int cbl = t / Zc, z = t - cbl * Zc;
+    const int par_lane = t & 1;               // edges k = 2kk + par_lane of every row
+    const int s = t >> 1;                     // slot (CB-major: cl * Zc + z)
+    const int cbl = s / Zc, z = s - cbl * Zc;
     const int cb = blockIdx.x * G + cbl;
-    const bool valid = cbl < G && cb < B;
+    const bool valid = cbl < G && cb < B && s < kCS;
     const int cl = valid ? cbl : 0;
-    const int tz = cl * Zc + z;
     const int zv = valid ? z : 0;
+    const int tz = cl * Zc + zv;
     const double* lrow = llr + (int64_t)(valid ? cb : 0) * ldl;
     int8_t* crow = ck + (int64_t)(valid ? cb : 0) * ldc;
-    double* mrow = msg + (int64_t)(valid ? cb : 0) * E * Zc;   // Lr[e][z]
-    auto rot = [&](int s) { int m = zv + s; return cl * Zc + (m >= Zc ? m - Zc : m); };   // (z+s) % Zc
-    auto llrx = [&](int i) { return lrow[(KB + i - pc) * Zc + zv]; };   // ext column of row i
-
-    if (valid) {
-        for (int j = 0; j < KC; ++j) app[j * kCS + tz] = j < pc ? 0.0 : lrow[(j - pc) * Zc + z];
-        for (int e = 0; e < E; ++e) mrow[e * Zc + z] = 0.0;   // Lr = 0 (:101)
-    }
-    if (valid && z == 0) flag[cl] = 0;
-    bool active = valid;
-    __syncthreads();
-
-    // r_old of the next row's first PF edges, loaded ahead (the rest at the row: registers)
-    constexpr int PF = DM < kBpPrefetch ? DM : kBpPrefetch;
-    double pf[PF];
-    // z made opaque per row / column pass: otherwise LICM hoists the hundreds of loop-invariant
-    // per-edge addresses out of the iteration loop into registers (hundreds of scratch spills)
+    double* mrow = msg + (int64_t)(valid ? cb : 0) * NPAIR * Zc * 2;   // [P][z][2]
+    // z / base pointers opaque per row or pass: otherwise LICM hoists the loop-invariant per-edge
+    // addresses out of the iteration loop into registers (hundreds of scratch spills)
     auto opaque_z = [&]() {
         int zo = zv;
         asm volatile("" : "+v"(zo));
         return zo;
     };
-    auto opaque_p = [&](auto* p) {   // the same for a row base pointer (no hoisted per-edge addresses)
+    auto opaque_p = [&](auto* p) {
         uint64_t v = (uint64_t)(uintptr_t)p;
         asm volatile("" : "+v"(v));
         return (decltype(p))(uintptr_t)v;
     };
+    // own core column entries for the LQ update: columns j = 2jj + par_lane
+    if (valid) {
+        for (int j = par_lane; j < KC; j += 2) {
+            app[j * kCS + tz] = j < pc ? 0.0 : lrow[(j - pc) * Zc + z];
+            acc[j * kCS + tz] = 0.0;
+        }
+        for (int q = 0; q < NPAIR; ++q) mrow[(q * Zc + z) * 2 + par_lane] = 0.0;   // Lr = 0 (:101)
+    }
+    if (valid && z == 0 && par_lane == 0) flag[cl] = 0;
+    bool active = valid;
+    __syncthreads();
+
+    double pf[KK];   // r_old of the next row's own edges, loaded ahead
     auto load_row = [&](int i, int zo, double* mr) {
-        const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0;
+        const int d = row_start_d<BG>(i + 1) - row_start_d<BG>(i), q0 = bp_pairs_d<BG>().ps[i];
 #pragma unroll
-        for (int k = 0; k < PF; ++k)
-            if (k < d) pf[k] = mr[(e0 + k) * Zc + zo];
+        for (int kk = 0; kk < KK; ++kk)
+            if (2 * kk < d) pf[kk] = mr[((q0 + kk) * Zc + zo) * 2 + par_lane];
     };
     int it = 0;
     for (; it < L; ++it) {
         bool fail = false;
-        uint64_t hdx = 0;
-        // ---- phase A (:117-123, _BP_process :145-176)
+        uint64_t hdx = 0;   // ext decisions (LQ_old < 0) of the rows whose ext edge is this lane's
         if (active) {
             load_row(0, opaque_z(), opaque_p(mrow));
             for (int i = 0; i < MB; ++i) {
+                if (bp_pairs_d<BG>().first[i] && i > 0) __syncthreads();   // next row group: ordered sums
                 const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0;
+                const int q0 = bp_pairs_d<BG>().ps[i];
                 const int zo = opaque_z();
                 double* const mr = opaque_p(mrow);
                 const double* const lr = opaque_p(lrow);
-                auto rotz = [&](int s) { int m = zo + s; return cl * Zc + (m >= Zc ? m - Zc : m); };
-                auto row = [&](auto dc) {
-                    constexpr int D = decltype(dc)::value;
-                    double tq[D];
-                    bool par = false;
+                auto rotz = [&](int sft) { int m = zo + sft; return cl * Zc + (m >= Zc ? m - Zc : m); };
+                double tq[KK];
 #pragma unroll
-                    for (int k = 0; k < D; ++k) tq[k] = k < PF ? pf[k] : mr[(e0 + k) * Zc + zo];   // r_old
-                    if (i + 1 < MB) load_row(i + 1, zo, mr);
-                    int nz = 0, zk = 0;
-                    double prod = 1.0, pb = 1.0, pa = 1.0;   // all; before / after the first zero
+                for (int kk = 0; kk < KK; ++kk) tq[kk] = pf[kk];   // r_old
+                if (i + 1 < MB) load_row(i + 1, zo, mr);
+                bool par = false;
+                int nz = 0, zk = 255;
+                double prod = 1.0, pnz = 1.0;   // product of all own t / of those with q != 0
+                int jcol[KK];
+                {
                     BpTanhK TK;
                     TK.load();
 #pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        const int e = e0 + k, j = col_d<BG>(e);
-                        const double rold = tq[k];
-                        double a;
-                        if (j < KC) {
-                            a = app[j * kCS + rotz(shift_of<BG>(zi, e))];
-                        } else {
-                            a = lr[(KB + i - pc) * Zc + zo] + rold;   // LQ of the degree-1 column
-                            hdx |= (uint64_t)(a < 0.0) << (i - 4);
+                    for (int kk = 0; kk < KK; ++kk) {
+                        const int k = 2 * kk + par_lane;
+                        jcol[kk] = -1;
+                        if (2 * kk < d) {   // wave-uniform: the pair's first edge exists
+                            const int ea = e0 + 2 * kk, eb = min(ea + 1, P::E - 1);
+                            const int j = par_lane ? col_d<BG>(eb) : col_d<BG>(ea);
+                            const int sft = par_lane ? shift_of<BG>(zi, eb) : shift_of<BG>(zi, ea);
+                            if (k < d) {
+                                const double rold = tq[kk];
+                                double a;
+                                if (j < KC) {
+                                    a = app[j * kCS + rotz(sft)];
+                                    jcol[kk] = j * kCS + rotz(sft);
+                                } else {
+                                    a = lr[(KB + i - pc) * Zc + zo] + rold;   // degree-1 column
+                                    hdx |= (uint64_t)(a < 0.0) << (i - 4);
+                                }
+                                par ^= a < 0.0;
+                                const double q = a - rold;   // Lq (:129-131)
+                                const double tk = bp_tanh_half(q, TK);   // tanh(q/2) (:152, :165)
+                                tq[kk] = tk;
+                                prod *= tk;
+                                if (q == 0.0) {
+                                    zk = nz == 0 ? k : zk;
+                                    ++nz;
+                                } else {
+                                    pnz *= tk;
+                                }
+                            }
                         }
-                        par ^= a < 0.0;
-                        const double q = a - rold;   // Lq (:129-131)
-                        const double tk = bp_tanh_half(q, TK);   // tanh(q / 2) (:152, :165)
-                        tq[k] = tk;
-                        __builtin_amdgcn_sched_barrier(0);   // one edge's temporaries at a time
-                        prod = k == 0 ? tk : prod * tk;   // np.prod: left to right
-                        if (q == 0.0) {
-                            if (nz == 0) zk = k;
-                            ++nz;
-                        } else if (nz == 0) {
-                            pb = k == 0 ? tk : pb * tk;
-                        } else {
-                            pa = k == zk + 1 ? tk : pa * tk;
-                        }
+                        __builtin_amdgcn_sched_barrier(0);
                     }
-                    fail |= par;
-                    const double pzero = pb * pa;   // prod(t[0:zk]) * prod(t[zk+1:])
+                }
+                // the pair's totals (np.prod order aside: even-edge x odd-edge partial products)
+                par ^= (pair_swap((uint32_t)par) & 1u) != 0;
+                fail |= par;
+                const uint32_t nzw = (uint32_t)nz | ((uint32_t)zk << 8), onzw = pair_swap(nzw);
+                const int nzt = nz + (int)(onzw & 0xff);
+                const int zkt = min(zk, (int)(onzw >> 8));
+                const double prodt = prod * pair_swap(prod);
+                const double pnzt = pnz * pair_swap(pnz);
+                {
                     BpAtanhK AK;
                     AK.load();
 #pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        double r;
-                        if (nz == 0) {
-                            const double tmp2 = prod / tq[k];
-                            r = tmp2 >= 1.0 ? kBpClip : (tmp2 <= -1.0 ? -kBpClip : bp_two_atanh(tmp2, AK));
-                        } else {
-                            r = (nz == 1 && k == zk) ? pzero : 0.0;
+                    for (int kk = 0; kk < KK; ++kk) {
+                        const int k = 2 * kk + par_lane;
+                        if (2 * kk < d) {
+                            double r = 0.0;
+                            if (k < d) {
+                                if (nzt == 0) {
+                                    const double tmp2 = prodt / tq[kk];
+                                    r = tmp2 >= 1.0 ? kBpClip : (tmp2 <= -1.0 ? -kBpClip : bp_two_atanh(tmp2, AK));
+                                } else if (nzt == 1 && k == zkt) {
+                                    r = pnzt;   // prod(t[0:zk]) * prod(t[zk+1:]) (:166-172)
+                                }
+                                if (jcol[kk] >= 0) acc[jcol[kk]] += r;   // rows of a group: disjoint columns
+                            }
+                            mr[((q0 + kk) * Zc + zo) * 2 + par_lane] = r;
                         }
-                        mr[(e0 + k) * Zc + zo] = r;
                         __builtin_amdgcn_sched_barrier(0);
                     }
-                };
-                switch (d) {   // wave-uniform
-#define LDPC5G_BP_DEG(D) \
-    case D:              \
-        if constexpr (bp_has_deg<BG>(D)) row(std::integral_constant<int, D>{}); \
-        break;
-                    LDPC5G_BP_DEG(3) LDPC5G_BP_DEG(4) LDPC5G_BP_DEG(5) LDPC5G_BP_DEG(6) LDPC5G_BP_DEG(7)
-                    LDPC5G_BP_DEG(8) LDPC5G_BP_DEG(9) LDPC5G_BP_DEG(10) LDPC5G_BP_DEG(19)
-#undef LDPC5G_BP_DEG
-                    default: __builtin_trap();
                 }
             }
             if (fail) flag[cl] = 1;
         }
-        __syncthreads();   // messages (global) and flags: visible to the workgroup
+        __syncthreads();   // flags, last group's sums
+        const uint32_t hx0 = pair_swap((uint32_t)hdx), hx1 = pair_swap((uint32_t)(hdx >> 32));
+        hdx |= ((uint64_t)hx1 << 32) | hx0;
         if (active && flag[cl] == 0) {   // syndrome of LQ at pass start was 0 (:107-114)
             const int zo = opaque_z();
             int8_t* const cr = opaque_p(crow);
-            for (int j = 0; j < KC; ++j) cr[j * Zc + zo] = (int8_t)(app[j * kCS + cl * Zc + zo] < 0.0);
-            for (int i = 4; i < MB; ++i) cr[(KB + i) * Zc + zo] = (int8_t)((hdx >> (i - 4)) & 1u);
-            if (z == 0) status[cb] = 1, iters[cb] = it;
+            for (int j = par_lane; j < KC; j += 2) cr[j * Zc + zo] = (int8_t)(app[j * kCS + cl * Zc + zo] < 0.0);
+            for (int i = 4 + par_lane; i < MB; i += 2) cr[(KB + i) * Zc + zo] = (int8_t)((hdx >> (i - 4)) & 1u);
+            if (z == 0 && par_lane == 0) status[cb] = 1, iters[cb] = it;
             active = false;
         }
-        // ---- phase B: LQ = LLRin + Lr.sum(axis=0) (:126), column by column, rows ascending
-        if (active)
-            sfor<0, KC>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                const int zo = opaque_z();
-                const double* const mr = opaque_p(mrow);
-                const double* const lr = opaque_p(lrow);
-                auto rotmz = [&](int s) { int m = zo - s; return m < 0 ? m + Zc : m; };   // (z-s) % Zc
-                constexpr int x0 = kCols<BG>.start[j], x1 = kCols<BG>.start[j + 1];
-                double v[x1 - x0];
-                sfor<x0, x1>([&](auto xc) {
-                    constexpr int e = kCols<BG>.edge[decltype(xc)::value];
-                    v[decltype(xc)::value - x0] = mr[e * Zc + rotmz(shift_of<BG>(zi, e))];
-                });
+        if (active) {   // LQ = LLRin + Lr.sum(axis=0) (:126) for the own entries; sums back to 0
+            const int zo = opaque_z();
+            const double* const lr = opaque_p(lrow);
+            for (int j = par_lane; j < KC; j += 2) {
+                const int x = j * kCS + cl * Zc + zo;
                 const double lf = j < pc ? 0.0 : lr[(j < pc ? 0 : j - pc) * Zc + zo];
-                double acc = 0.0;
-#pragma unroll
-                for (int x = 0; x < x1 - x0; ++x) acc = acc + v[x];
-                app[j * kCS + tz] = lf + acc;
-                __builtin_amdgcn_sched_barrier(0);   // one column's loads in flight at a time
-            });
+                app[x] = lf + acc[x];
+                acc[x] = 0.0;
+            }
+        }
         __syncthreads();
-        if (valid && z == 0) flag[cl] = 0;
+        if (valid && z == 0 && par_lane == 0) flag[cl] = 0;
         if (!__syncthreads_or(active)) break;
     }
     // ---- exhausted: ck = LQ <= 0, status = syndrome == 0 (:133-143)
@@ -413,30 +474,28 @@ __global__ __launch_bounds__(kBpThreads, 3) void ldpc_bp_kernel(
     double* const mr = opaque_p(mrow);
     const double* const lr = opaque_p(lrow);
     int8_t* const cr = opaque_p(crow);
-    auto rotf = [&](int s) { int m = zo + s; return cl * Zc + (m >= Zc ? m - Zc : m); };
+    auto rotf = [&](int sft) { int m = zo + sft; return cl * Zc + (m >= Zc ? m - Zc : m); };
     if (active) {
         bool fail = false;
         for (int i = 0; i < MB; ++i) {
-            const int e0 = row_start_d<BG>(i), e1 = row_start_d<BG>(i + 1);
+            const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0, q0 = bp_pairs_d<BG>().ps[i];
             bool par = false;
-            for (int e = e0; e < e1; ++e) {
-                const int j = col_d<BG>(e);
+            for (int k = par_lane; k < d; k += 2) {
+                const int e = e0 + k, j = col_d<BG>(e);
                 const double a = j < KC ? app[j * kCS + rotf(shift_of<BG>(zi, e))]
-                                        : lr[(KB + i - pc) * Zc + zo] + mr[e * Zc + zo];
+                                        : lr[(KB + i - pc) * Zc + zo] + mr[((q0 + k / 2) * Zc + zo) * 2 + par_lane];
                 par ^= a <= 0.0;
+                if (j >= KC) cr[(KB + i) * Zc + zo] = (int8_t)(a <= 0.0);   // the ext decision
             }
+            par ^= (pair_swap((uint32_t)par) & 1u) != 0;
             fail |= par;
         }
         if (fail) flag[cl] = 1;
     }
     __syncthreads();
     if (active) {
-        for (int j = 0; j < KC; ++j) cr[j * Zc + zo] = (int8_t)(app[j * kCS + cl * Zc + zo] <= 0.0);
-        for (int i = 4; i < MB; ++i) {
-            const int el = row_start_d<BG>(i + 1) - 1;   // the ext column is the row's last edge
-            cr[(KB + i) * Zc + zo] = (int8_t)(lr[(KB + i - pc) * Zc + zo] + mr[el * Zc + zo] <= 0.0);
-        }
-        if (z == 0) status[cb] = flag[cl] == 0, iters[cb] = L;
+        for (int j = par_lane; j < KC; j += 2) cr[j * Zc + zo] = (int8_t)(app[j * kCS + cl * Zc + zo] <= 0.0);
+        if (z == 0 && par_lane == 0) status[cb] = flag[cl] == 0, iters[cb] = L;
     }
 }
 
@@ -458,9 +517,10 @@ int launch_bp_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
     using P = BGT<BG>;
     auto kern = ldpc_bp_kernel<BG>;
     const int G = dec_G(Zc);
-    const size_t lds = (size_t)P::KC * kCS * sizeof(double) + kCS * sizeof(int);   // 2 workgroups / CU
+    // LQ image + row-ascending sums of the core columns, flags: one workgroup per CU
+    const size_t lds = (size_t)2 * P::KC * kCS * sizeof(double) + kCS * sizeof(int);
     if (int rc = set_lds_once<ldpc_bp_kernel<BG>>(lds)) return rc;
-    const int threads = ((G * Zc + 63) / 64) * 64;
+    const int threads = ((2 * G * Zc + 63) / 64) * 64;
     hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(threads), lds, st, llr, ck, status, iters,
                        msg, B, Zc, zi, G, ldl, ldc, L, pc);
     return check_hip(hipGetLastError(), "ldpc_bp_kernel launch");
@@ -485,5 +545,7 @@ int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* 
 }
 
 int edges_of_bg(int bgn) { return bgn == 1 ? BGT<1>::E : BGT<2>::E; }
+
+int bp_scratch_per_zc(int bgn) { return 2 * (bgn == 1 ? kBpPairs<1>.np : kBpPairs<2>.np); }
 
 }  // namespace ldpc5g_impl

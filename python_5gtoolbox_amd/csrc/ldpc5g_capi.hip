@@ -430,7 +430,7 @@ int ldpc5g_decode_bf(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* st
 
 int64_t ldpc5g_bp_scratch_elems(int32_t B, int32_t bgn, int32_t Zc) {
     if ((bgn != 1 && bgn != 2) || B < 0 || zc_index(Zc) < 0) return -1;
-    return (int64_t)B * edges_of_bg(bgn) * Zc;
+    return (int64_t)B * bp_scratch_per_zc(bgn) * Zc;
 }
 
 int ldpc5g_decode_bp(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

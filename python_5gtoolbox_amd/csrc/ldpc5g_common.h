@@ -185,6 +185,8 @@ int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* 
               double* msg, int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc,
               hipStream_t st);
 int edges_of_bg(int bgn);
+// BP message scratch per codeblock, in units of Zc doubles (2 x the row-edge pair slots)
+int bp_scratch_per_zc(int bgn);
 
 // ---- arbitrary parity-check matrices (ldpc5g_sparse.hip): CSR rows (edges in ascending column
 // order) + CSC columns (entries in ascending row order: edge id and row)
