@@ -359,7 +359,9 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
         if (active) {
             load_row(0, opaque_z(), opaque_p(mrow));
             for (int i = 0; i < MB; ++i) {
-                if (bp_pairs_d<BG>().first[i] && i > 0) __syncthreads();   // next row group: ordered sums
+                // next row group: the LDS sums ordered.  An LDS-only barrier: __syncthreads() would
+                // also wait (vmcnt(0)) for the next row's message loads and this row's stores
+                if (bp_pairs_d<BG>().first[i] && i > 0) lds_sync();
                 const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0;
                 const int q0 = bp_pairs_d<BG>().ps[i];
                 const int zo = opaque_z();
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
             }
             if (fail) flag[cl] = 1;
         }
-        __syncthreads();   // flags, last group's sums
+        lds_sync();   // flags, last group's sums (LDS only; messages are per lane)
         const uint32_t hx0 = pair_swap((uint32_t)hdx), hx1 = pair_swap((uint32_t)(hdx >> 32));
         hdx |= ((uint64_t)hx1 << 32) | hx0;
         if (active && flag[cl] == 0) {   // syndrome of LQ at pass start was 0 (:107-114)
