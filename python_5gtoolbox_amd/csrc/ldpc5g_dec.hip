@@ -17,6 +17,9 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
     if (layered)
         return dead ? launch_dec_l_dead(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                     : launch_dec_l(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+    // a few large float64 codeblocks (the per-codeblock drop-ins): each over several CUs
+    if (dtype == LDPC5G_F64 && split_wanted(bgn, B, Zc))
+        return launch_flood_split(bgn, (const double*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     // launches whose codeblocks fit 64 slots (one small codeblock per drop-in call): 16 parts
     const int G = std::min(dec_G(Zc, false), B);
     if (G * Zc <= kFloodSmallCS)

@@ -1,0 +1,404 @@
+// ldpc5g_dec_split.hip — float64 flooding min-sum decoder for a FEW LARGE codeblocks: the launch
+// shape of the per-codeblock drop-ins at Zc >= 64 (nr_decode_ldpc decodes one codeblock per call, so
+// its latency is one codeblock's, not a batch's).  Each codeblock is spread over
+// W = ceil(MB * ceil(Zc/64) / 16) workgroups of 1024 threads, one per CU (W = 18 for BG1 Zc = 384), instead of
+// the batch kernel's one workgroup per codeblock.
+//
+// Same arithmetic in the same order as the small-codeblock kernel (ldpc5g_dec_small.h), hence
+// bit-identical to py5gphy/ldpc/nr_ldpc_decode.py:51-143 with _min_sum_process :178-227:
+//   phase A  a thread per check node (base row i, z): reads LQ_old of its row's edges at
+//            (z + V) mod Zc, the syndrome of LQ_old's hard decisions (:107-114) from the same reads,
+//            new row state (:117-123, :186-202), and its core edges' new messages r written to their
+//            message slots in CSC order (column j's edges rows ascending) at row (z + V) mod Zc;
+//   phase B  a thread per core column entry (j, z): LQ = LLRin + the column's messages summed rows
+//            ascending (Lr.sum(axis=0), :126) — consecutive slots, all loads in flight together.
+// LQ and the messages live in a global scratch (per codeblock (KC + NCE) * Zc doubles, 0.84 MB for
+// BG1 Zc = 384) instead of LDS, and the two barriers per iteration are barriers over the codeblock's
+// W workgroups: one monotonic counter per codeblock; every hand-off store (LQ, messages, flags) is an
+// `sc1` (write-through) store, every storing wave drains (vmcnt(0)) before the workgroup barrier
+// behind which one lane adds to the counter, the counter is polled with an `sc1` load and every load
+// of hand-off data is an `sc1` global load (MI355X_MICROARCH.md, hand-off table first row): no L2
+// write-back or L1 invalidate fence on the critical path.  All W*B workgroups must be resident
+// together: the launcher keeps B*W <= kSplitMaxWG (half the CUs) and one workgroup per CU.
+#include <stdlib.h>
+
+#include "ldpc5g_dec_small.h"
+
+namespace ldpc5g_impl {
+namespace {
+
+constexpr int kSplitThreads = 1024;
+constexpr int kSplitSync = 64;   // sync words per codeblock (a 256-B line): barrier counter, flags
+constexpr int kSplitMaxWG = 128;
+// loads in flight per chunk (phase A LQ reads, phase B message reads); 32: a row's / column's all
+// at once (r05, one BG1 Zc=384 codeblock: 10 / 10 100 us per call, all 87 us)
+#ifndef LDPC5G_SPLIT_CH
+#define LDPC5G_SPLIT_CH 32
+#endif
+#ifndef LDPC5G_SPLIT_CCH
+#define LDPC5G_SPLIT_CCH 32
+#endif
+// development instrumentation (tools/split_probe.py): workgroup 0 thread 0's real-time clock
+// (100 MHz) at phase boundaries, dumped over codeblock 0's decisions
+#ifdef LDPC5G_SPLIT_TS
+#define SPLIT_TS(n) \
+    if (g == 0 && (n) < 16) tsv[(n)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define SPLIT_TS(n)
+#endif
+
+template <int BG>
+constexpr int split_rows() { return BGT<BG>::KC + kSmallPlanH<BG>.ncore; }   // scratch rows of Zc doubles
+
+using g_f64 = __attribute__((address_space(1))) double;
+using g_u32 = __attribute__((address_space(1))) uint32_t;
+
+// hand-off loads / stores: global (not flat) sc1 accesses
+__device__ __forceinline__ double ld_sc1(const double* base, uint32_t byte) {
+    return __hip_atomic_load((g_f64*)((uintptr_t)base + byte), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* base, uint32_t byte, double v) {
+    __hip_atomic_store((g_f64*)((uintptr_t)base + byte), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load((g_u32*)(uintptr_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Work split.  A wave owns one CHUNK: 64 consecutive slots z of one base row (phase A) and of one
+// core column (phase B), so a row's / column's degree is wave-uniform and a wave issues exactly its
+// edges' loads.  The chunks are dealt to the W workgroups in degree-descending order, snake-wise
+// (wave v of workgroup w takes chunk v*W + w, or v*W + W-1-w for odd v), so every workgroup moves
+// about the same number of bytes per phase: the barriers wait for the slowest workgroup, and a
+// CU's remote-load bandwidth, not its ALUs, bounds a phase (measured r05: with rows / columns in
+// natural order workgroup 0 alone held the degree-19 rows and the degree-30 column).
+template <int BG>
+struct SplitPlan {
+    int8_t rord[BGT<BG>::MB] = {};   // base rows, degree descending (ties: ascending index)
+    int8_t cord[BGT<BG>::KC] = {};   // core columns, degree descending
+    constexpr SplitPlan() {
+        using P = BGT<BG>;
+        bool used[P::MB] = {};
+        for (int n = 0; n < P::MB; ++n) {
+            int b = -1;
+            for (int i = 0; i < P::MB; ++i)
+                if (!used[i] && (b < 0 || P::RS[i + 1] - P::RS[i] > P::RS[b + 1] - P::RS[b])) b = i;
+            used[b] = true, rord[n] = (int8_t)b;
+        }
+        bool cu[P::KC] = {};
+        constexpr SmallPlan<BG> sp{};
+        for (int n = 0; n < P::KC; ++n) {
+            int b = -1;
+            for (int j = 0; j < P::KC; ++j)
+                if (!cu[j] && (b < 0 || sp.cstart[j + 1] - sp.cstart[j] > sp.cstart[b + 1] - sp.cstart[b])) b = j;
+            cu[b] = true, cord[n] = (int8_t)b;
+        }
+    }
+};
+template <int BG>
+__device__ constexpr SplitPlan<BG> kSplitPlanD{};
+
+template <int BG, bool OFS>
+__global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
+    const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int Zc, int zi, int W, int64_t ldl, int64_t ldc, int L, double alpha,
+    double beta, int pc, double* __restrict__ scratch, uint32_t* __restrict__ sync) {
+    using P = BGT<BG>;
+    using T = double;
+    constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = 8;
+    constexpr int DMAX = kSmallPlanH<BG>.dmax, CMAX = kSmallPlanH<BG>.cmax;
+    constexpr int CH = LDPC5G_SPLIT_CH, CCH = LDPC5G_SPLIT_CCH;   // loads in flight per chunk: phase A, B
+    __shared__ uint32_t rws[MB * DMAX], wws[MB * DMAX];   // edge words per (row, edge < DMAX)
+    __shared__ uint32_t lfail, lflag;
+
+    const int cb = blockIdx.x / W, w = blockIdx.x - cb * W;
+    const int t = threadIdx.x, lane = t & 63;
+    const int v = __builtin_amdgcn_readfirstlane(t >> 6);
+#ifdef LDPC5G_SPLIT_TS
+    uint64_t tsv[16] = {};
+#endif
+    const int g = w * kSplitThreads + t;   // (instrumentation: workgroup 0, thread 0)
+    SPLIT_TS(0);
+    const T* lrow = llr + (int64_t)cb * ldl;
+    int8_t* crow = ck + (int64_t)cb * ldc;
+    const uint32_t ZT = (uint32_t)(Zc * TS);
+    double* lq = scratch + (size_t)cb * split_rows<BG>() * Zc;   // [KC][Zc] LQ of the core columns
+    double* msg = lq + (size_t)KC * Zc;                            // [NCE][Zc] messages, CSC slots
+    uint32_t* sy = sync + cb * kSplitSync;   // [0] barrier counter, [1] fail tag, [2] final fail
+
+    // barrier over the codeblock's W workgroups.  sig: this workgroup's fail tag (LDS lfail) is
+    // raised into sy[fi] first; afterwards lflag = sy[fi] for every thread of the workgroup.
+    uint32_t nbar = 0;
+    auto grid_sync = [&](int fi, uint32_t sig) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's hand-off stores done
+        __syncthreads();
+        nbar += (uint32_t)W;
+        if (t == 0) {
+            if (sig != 0u && lfail == sig) {
+                __hip_atomic_fetch_max((g_u32*)(uintptr_t)(sy + fi), sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __hip_atomic_fetch_add((g_u32*)(uintptr_t)sy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (ld_sc1(sy) < nbar) __builtin_amdgcn_s_sleep(1);
+            lflag = ld_sc1(sy + fi);
+        }
+        __syncthreads();
+    };
+
+    // ---- edge words: read word = column byte offset | (V mod Zc)*8 << 17; write word = CSC slot
+    //      byte offset | (V mod Zc)*8 << 20
+    for (int q = t; q < MB * DMAX; q += kSplitThreads) {
+        const int i = q / DMAX, x = q - i * DMAX;
+        const int e0 = row_start_d<BG>(i), dc = row_start_d<BG>(i + 1) - e0 - (i >= 4 ? 1 : 0);
+        uint32_t rw = 0u, ww = 0u;
+        if (x < dc) {
+            const uint32_t w0 = kSmallPlanD<BG>.ew[e0 + x];
+            const uint32_t sb = (uint32_t)shift_of<BG>(zi, e0 + x) * TS;
+            rw = (w0 & 0xffu) * ZT | (sb << 17);
+            ww = (w0 >> 8) * ZT | (sb << 20);
+        }
+        rws[q] = rw, wws[q] = ww;
+    }
+    if (t == 0) lfail = 0u;
+    const int nch = (Zc + 63) >> 6;   // chunks per row / column
+    const int ch = v * W + ((v & 1) ? W - 1 - w : w);   // this wave's chunk (rank in degree order)
+    // own core column entry (cj, cz): LLR, CSC range (column-uniform: SGPRs)
+    const bool hasc_w = ch < KC * nch;
+    const int cj = hasc_w ? kSplitPlanD<BG>.cord[ch / nch] : 0;
+    const int cz = (ch % nch) * 64 + lane;
+    const bool hasc = hasc_w && cz < Zc;
+    const int cn = kSmallPlanD<BG>.cstart[cj + 1] - kSmallPlanD<BG>.cstart[cj];
+    const uint32_t cr0 = (uint32_t)kSmallPlanD<BG>.cstart[cj] * ZT + (uint32_t)cz * TS;
+    const uint32_t cq = (uint32_t)cj * ZT + (uint32_t)cz * TS;   // LQ entry
+    const bool cpun = cj < pc;
+    const T lf = (hasc && !cpun) ? lrow[(cj - pc) * Zc + cz] : T(0);
+    T lqv = lf;
+    if (hasc) st_sc1(lq, cq, lf);
+    // own check node (ri, rz): row state (nA, nB, signs | argmin << 24), extension LLR
+    const bool hasn_w = ch < MB * nch;
+    const int ri = hasn_w ? kSplitPlanD<BG>.rord[ch / nch] : 0;
+    const int rz = (ch % nch) * 64 + lane;
+    const bool hasn = hasn_w && rz < Zc;
+    const uint32_t zb0 = (uint32_t)rz * TS, re0 = (uint32_t)(ri * DMAX);
+    const int rd = row_start_d<BG>(ri + 1) - row_start_d<BG>(ri);
+    const bool xe = ri >= 4;   // rows >= 4: the last edge is the extension column
+    const int dc = rd - (xe ? 1 : 0);
+    const T xl = (hasn && xe) ? lrow[(KB + ri - pc) * Zc + rz] : T(0);
+    T nA = T(0), nB = T(0);
+    uint32_t wd = 0u;
+    uint32_t mv = 0x80000000u;
+    asm volatile("" : "+v"(mv));
+    grid_sync(1, 0u);
+    SPLIT_TS(1);
+
+    bool hdx = false;
+    int it = 0;
+    for (; it < L; ++it) {
+        // ---- phase A (rows from LQ_old, syndrome of LQ_old): the wave's row, its dc core edges
+        bool fail = false;
+        // per-iteration opaque copies: the addresses are loop-invariant, and hoisting them out of the
+        // iteration loop (~40 extra live VGPRs) spills
+        uint32_t zb = zb0, cr = cr0;
+        asm volatile("" : "+v"(zb), "+v"(cr));
+        if (hasn) {
+            uint32_t u = wd << (32 - rd);
+            const uint32_t idxo = wd >> 24;
+            const T mA = nA, mB = nB;
+            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+            uint32_t idx = 0, negs = 0;
+            bool par = false;
+            auto edge = [&](uint32_t q0, T av, T rold) {
+                par ^= av < T(0);
+                const T q = av - rold;
+                const T aq = fabs(q);
+                idx = aq < min1 ? q0 : idx;
+                asm volatile("" : "+v"(idx));
+                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                two_min(min1, min2, aq);
+            };
+            // the row's LQ reads CH at a time, a chunk's all in flight before the first is used
+            sfor<0, (DMAX + CH - 1) / CH>([&](auto cc) {
+                constexpr int c0 = decltype(cc)::value * CH, c1 = c0 + CH < DMAX ? c0 + CH : DMAX;
+                if (c0 < dc) {
+                    T a[CH];
+                    sfor<c0, c1>([&](auto xc) {
+                        constexpr int x = decltype(xc)::value;
+                        if (x < dc) {
+                            const uint32_t Wx = rws[re0 + x];
+                            const uint32_t zz = zb + (Wx >> 17);
+                            a[x - c0] = ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT));
+                        }
+                    });
+                    sfor<c0, c1>([&](auto xc) {
+                        constexpr int x = decltype(xc)::value;
+                        if (x < dc) {
+                            const T rold = xsign_v(idxo == (uint32_t)x ? mB : mA, u, mv);
+                            asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1
+                            edge((uint32_t)x, a[x - c0], rold);
+                        }
+                    });
+                }
+            });
+            if (xe) {   // the extension edge (the row's last): LQ of the degree-1 column = LLR + its r
+                const T rold = xsign_v(idxo == (uint32_t)dc ? mB : mA, wd << 31, mv);
+                const T av = xl + rold;
+                hdx = av < T(0);
+                edge((uint32_t)dc, av, rold);
+            }
+            fail = par;
+            T x1 = min1, x2 = min2;
+            if constexpr (OFS) {
+                x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
+                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const uint32_t sgn = 0u - (__builtin_popcount(negs) & 1u);   // row sign product
+            const uint32_t flip = sgn & ((1u << rd) - 1u);
+            nA = alpha * x1, nB = alpha * x2;
+            wd = (negs ^ flip) | (idx << 24);
+            uint32_t un = wd << (32 - rd);
+            sfor<0, DMAX>([&](auto xc) {
+                constexpr int x = decltype(xc)::value;
+                if (x < dc) {
+                    const uint32_t V = wws[re0 + x];
+                    const T r = xsign_v(idx == (uint32_t)x ? nB : nA, un, mv);
+                    asm("v_add_u32 %0, %1, %1" : "=v"(un) : "v"(un));
+                    const uint32_t zz = zb + (V >> 20);
+                    st_sc1(msg, (V & 0xfffffu) + min(zz, zz - ZT), r);
+                }
+            });
+        }
+        if (fail) lfail = (uint32_t)(it + 1);
+        if (it < 2) SPLIT_TS(2 + 4 * it);
+        grid_sync(1, (uint32_t)(it + 1));
+        if (it < 2) SPLIT_TS(3 + 4 * it);
+        if (lflag != (uint32_t)(it + 1)) {
+            // ---- the syndrome of LQ_old holds (:112-114): its hard decisions are the output
+            if (hasc) crow[cj * Zc + cz] = (int8_t)(lqv < T(0));
+            if (hasn && xe) crow[(KB + ri) * Zc + rz] = (int8_t)hdx;
+            if (w == 0 && t == 0) status[cb] = 1, iters[cb] = it;
+            return;
+        }
+        // ---- phase B: LQ = LLRin + Lr.sum(axis=0) (:126), rows ascending: the wave's column
+        if (hasc) {
+            T acc = T(0);
+            sfor<0, (CMAX + CCH - 1) / CCH>([&](auto cc) {
+                constexpr int p0 = decltype(cc)::value * CCH, p1 = p0 + CCH < CMAX ? p0 + CCH : CMAX;
+                if (p0 < cn) {
+                    T m[CCH];
+                    sfor<p0, p1>([&](auto pc_) {
+                        constexpr int p = decltype(pc_)::value;
+                        if (p < cn) m[p - p0] = ld_sc1(msg, cr + (uint32_t)p * ZT);
+                    });
+                    sfor<p0, p1>([&](auto pc_) {
+                        constexpr int p = decltype(pc_)::value;
+                        if (p < cn) acc = acc + m[p - p0];
+                    });
+                }
+            });
+            lqv = (cpun ? T(0) : lf) + acc;   // punctured columns: LLR 0 (:43)
+            st_sc1(lq, cq, lqv);
+        }
+        if (it < 2) SPLIT_TS(4 + 4 * it);
+        grid_sync(1, 0u);
+        if (it < 2) SPLIT_TS(5 + 4 * it);
+    }
+
+    // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
+    SPLIT_TS(10);
+    bool ox = false;
+    if (hasn) {
+        bool par = false;
+        if (xe) {
+            const T rx = xsign_v((wd >> 24) == (uint32_t)dc ? nB : nA, wd << 31, mv);
+            ox = xl + rx <= T(0);
+            par = ox;
+        }
+        sfor<0, DMAX>([&](auto xc) {
+            constexpr int x = decltype(xc)::value;
+            if (x < dc) {
+                const uint32_t Wx = rws[re0 + x];
+                const uint32_t zz = zb0 + (Wx >> 17);
+                par ^= ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT)) <= T(0);
+            }
+        });
+        if (par) lfail = (uint32_t)(L + 1);
+    }
+    SPLIT_TS(11);
+    // ---- the decisions need no barrier; the status does: every workgroup raises its fail flag and
+    //      then adds to the counter, and the workgroup whose add comes last (told by the value the
+    //      add returns) reads the flag and writes the status — nobody waits
+    if (hasc) crow[cj * Zc + cz] = (int8_t)(lqv <= T(0));
+    if (hasn && xe) crow[(KB + ri) * Zc + rz] = (int8_t)ox;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        if (lfail == (uint32_t)(L + 1)) {
+            __hip_atomic_fetch_max((g_u32*)(uintptr_t)(sy + 2), (uint32_t)(L + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t old = __hip_atomic_fetch_add((g_u32*)(uintptr_t)sy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == nbar + (uint32_t)W) status[cb] = ld_sc1(sy + 2) == 0u, iters[cb] = L;
+    }
+    SPLIT_TS(12);
+#ifdef LDPC5G_SPLIT_TS
+    SPLIT_TS(13);
+    __syncthreads();
+    if (g == 0) for (int q_ = 0; q_ < 16; ++q_) ((uint64_t*)crow)[q_] = tsv[q_];
+#endif
+}
+
+template <int BG>
+int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
+                   int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                   hipStream_t st) {
+    const int W = split_parts(BG, Zc);
+    if (B * W > kSplitMaxWG) return fail(LDPC5G_ESIZE, "split decoder: %d x %d workgroups", B, W);
+    static std::atomic<uint64_t> pool_set{0};   // keep freed pool memory mapped (per device)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (!(pool_set.load(std::memory_order_acquire) & (1ull << (dev & 63)))) {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+        pool_set.fetch_or(1ull << (dev & 63), std::memory_order_release);
+    }
+    const size_t data = (size_t)B * split_rows<BG>() * Zc * sizeof(double);
+    const size_t bytes = data + (size_t)B * kSplitSync * 4;
+    void* p = nullptr;
+    if (int rc = check_hip(hipMallocAsync(&p, bytes, st), "hipMallocAsync (split decoder scratch)")) return rc;
+    uint32_t* sync = (uint32_t*)((char*)p + data);
+    int rc = check_hip(hipMemsetAsync(sync, 0, (size_t)B * kSplitSync * 4, st), "hipMemsetAsync");
+    if (!rc) {
+        auto kern = beta != 0.0 ? ldpc_split_kernel<BG, true> : ldpc_split_kernel<BG, false>;
+        hipLaunchKernelGGL(kern, dim3(B * W), dim3(kSplitThreads), 0, st, llr, ck, status, iters, Zc, zi, W,
+                           ldl, ldc, L, alpha, beta, pc, (double*)p, sync);
+        rc = check_hip(hipGetLastError(), "ldpc_split_kernel launch");
+    }
+    const int rf = check_hip(hipFreeAsync(p, st), "hipFreeAsync");
+    return rc ? rc : rf;
+}
+
+}  // namespace
+
+int split_parts(int bgn, int Zc) {   // 64-slot row chunks over 16-wave workgroups
+    const int mb = bgn == 1 ? BGT<1>::MB : BGT<2>::MB;
+    return (mb * ((Zc + 63) / 64) + kSplitThreads / 64 - 1) / (kSplitThreads / 64);
+}
+
+bool split_wanted(int bgn, int B, int Zc) {
+    // LDPC5G_NO_SPLIT=1: the one-workgroup-per-codeblock kernels instead (A/B measurements)
+    static const bool off = [] { const char* e = getenv("LDPC5G_NO_SPLIT"); return e && *e && *e != '0'; }();
+    // BG2 Zc <= 64 keeps the small-codeblock kernel (its LDS image fits one CU)
+    if (off || Zc < 64 || (bgn == 2 && Zc <= 64)) return false;
+    return B * split_parts(bgn, Zc) <= kSplitMaxWG;
+}
+
+int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
+                       int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta,
+                       int pc, hipStream_t st) {
+    return bgn == 1 ? launch_split_t<1>(llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
+                    : launch_split_t<2>(llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
+}
+
+}  // namespace ldpc5g_impl

@@ -226,7 +226,7 @@ def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
     mixed SNRs, and rate-matched rows (untransmitted extension columns +0.0: the dead-row
     variants), bit-exact with the oracle."""
     rng = np.random.default_rng(7 + rm + 10 * bg)
-    Zc, B = 384, 7
+    Zc, B = 384, 9   # float64: 9 codeblocks run the batch kernels (7 would take the split kernel)
     ck = rng.integers(0, 2, (B, (22 if bg == 1 else 10) * Zc)).astype(np.int8)
     dn = O.encode(ck, bg)
     snr = rng.choice([-1.0, 1.0, 3.0], size=B)[:, None]
@@ -239,6 +239,36 @@ def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
            else O.decode_flooding(llr, Zc, bg, 6, 1.0, 0.5, dtype))
     for g, r in zip(got, ref):
         assert np.array_equal(g, r)
+
+
+@pytest.mark.parametrize("bg,Zc,B", [(1, 384, 1), (2, 384, 1), (1, 384, 7), (1, 64, 1), (1, 96, 2),
+                                     (2, 72, 1), (2, 176, 3), (1, 208, 1), (2, 384, 8)])
+def test_decode_split_kernel_vs_oracle(torch, dec, bg, Zc, B):
+    """The multi-workgroup float64 flooding kernel (ldpc5g_dec_split.hip: each codeblock over
+    ceil(MB*Zc/1024) CUs, barriers over a codeblock's workgroups) that serves launches of a few
+    large codeblocks (the per-codeblock drop-ins), bit-exact with the oracle: NMS and OMS,
+    L = 0 / 1 / 8, integer LLRs (|q| ties), an all-zero codeblock, a noiseless one, mixed SNRs
+    (codeblocks of one launch exiting at different iterations) and rate-matched rows."""
+    rng = np.random.default_rng(Zc * 3 + B + 100 * bg)
+    K = (22 if bg == 1 else 10) * Zc
+    ck = rng.integers(0, 2, (B, K)).astype(np.int8)
+    dn = O.encode(ck, bg)
+    snr = rng.uniform(-3.0, 3.0, (B, 1))
+    noisy = 2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) / 10 ** (-snr / 10)
+    ties = ((1 - 2 * dn) * 2.0 + rng.integers(-3, 4, dn.shape)).astype(np.float64)
+    ties[0] = 0.0
+    if B > 1:
+        ties[1] = (1 - 2 * dn[1]) * 4.0
+    for llr in (noisy, ties):
+        for L, alpha, beta, rm in ((0, 0.75, 0.0, False), (1, 1.0, 0.5, False), (8, 0.75, 0.0, False),
+                                   (8, 1.0, 0.25, False), (6, 0.8, 0.0, True)):
+            x = llr.copy()
+            if rm:
+                x[:, -7 * Zc:] = 0
+            got = dec.nr_decode_ldpc_batch(x, Zc, bg, L, "min-sum", alpha, beta, "flooding", rate_matched=rm)
+            ref = O.decode_flooding(x, Zc, bg, L, alpha, beta, np.float64)
+            for g, r in zip(got, ref):
+                assert np.array_equal(g, r), (L, alpha, beta, rm)
 
 
 def test_decode_ldpc_full_length(torch, dec):

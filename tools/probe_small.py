@@ -33,7 +33,8 @@ def main():
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
     for bg, Zc, B, snr in [(2, 8, 1, 1.0), (2, 8, 1, -3.0), (1, 8, 1, -3.0), (2, 16, 1, -3.0),
-                           (2, 64, 1, -3.0), (2, 8, 8, -3.0), (1, 384, 1, -3.0)]:
+                           (2, 64, 1, -3.0), (2, 8, 8, -3.0), (1, 64, 1, -3.0), (1, 128, 1, -3.0),
+                           (1, 384, 1, -3.0), (1, 384, 1, 1.0), (2, 384, 1, -3.0), (1, 384, 4, -3.0)]:
         K, N, Nf = code_dims(bg, Zc)
         ck = torch.randint(0, 2, (B, K), dtype=torch.int8, device="cuda", generator=g)
         dn = E.encode_ldpc_batch(ck, bg)
