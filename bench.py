@@ -316,6 +316,44 @@ def bench_dlsch_caller(rank, reps=5):
             "codec_only_ms_per_codeblock": round(res["codec_only_swap_ms_per_tb"] / 23, 3)}
 
 
+def bench_single_cb(torch, rank):
+    """One large codeblock per call (the per-codeblock drop-ins' shape at Zc=384, DLSCHDecode's
+    loop): float64 flooding NMS alpha=0.75 L=8 at -3 dB (all 8 iterations run), the multi-workgroup
+    kernel (ldpc5g_dec_split.hip: one codeblock over 18 CUs for BG1).  Device-resident call
+    (nr_decode_ldpc_batch, event-timed on the stream, scratch allocation included) and the numpy
+    drop-in nr_decode_ldpc (host wall, host<->device copies included)."""
+    import numpy as np
+    from python_5gtoolbox_amd import nr_ldpc_decode as D, nr_ldpc_encode as E
+    from python_5gtoolbox_amd.ldpc_info import code_dims
+    res = {"workload": "one BG1/BG2 Zc=384 codeblock per call, float64 flooding NMS alpha=0.75 L=8, -3 dB"}
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 + rank)
+    for bg in (1, 2):
+        Zc = 384
+        K, N, Nf = code_dims(bg, Zc)
+        ck = torch.randint(0, 2, (1, K), dtype=torch.int8, device="cuda", generator=g)
+        dn = E.encode_ldpc_batch(ck, bg)
+        sigma = 10 ** (3 / 20)
+        llr = (2 * ((1 - 2 * dn.double()) + sigma * torch.randn(dn.shape, dtype=torch.float64, device="cuda",
+                                                                  generator=g)) / sigma ** 2).contiguous()
+        out = (torch.empty((1, Nf), dtype=torch.int8, device="cuda"), torch.empty((1,), dtype=torch.uint8, device="cuda"),
+               torch.empty((1,), dtype=torch.int32, device="cuda"))
+        fn = lambda: D.nr_decode_ldpc_batch(llr, Zc, bg, 8, "min-sum", 0.75, 0.0, "flooding", out=out)  # noqa: E731
+        for _ in range(10):
+            fn()
+        us = ev_ms(torch, fn, reps=200) * 1e3
+        x = llr[0].cpu().numpy()
+        for _ in range(5):
+            D.nr_decode_ldpc(x, Zc, bg, 8, "min-sum", 0.75, 0.0)
+        t0 = time.perf_counter()
+        for _ in range(50):
+            D.nr_decode_ldpc(x, Zc, bg, 8, "min-sum", 0.75, 0.0)
+        host_us = (time.perf_counter() - t0) / 50 * 1e6
+        res[f"bg{bg}"] = {"device_us_per_call": round(us, 1), "dropin_host_us_per_call": round(host_us, 1),
+                          "iterations": int(out[2].item())}
+    return res
+
+
 def ev_ms(torch, fn, reps=5):
     """Event-timed milliseconds per call of fn (one untimed call first), on torch's current
     stream — the stream the library launches on."""
@@ -868,6 +906,7 @@ def main():
         del ckh, dnh
         ex["config1_per_codeblock"] = bench_config1(rank)
         ex["dlsch_caller_shape"] = bench_dlsch_caller(rank)
+        ex["single_codeblock_latency"] = bench_single_cb(torch, rank)
         tm = {}
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded
         if world == 1 or dist.get_backend() == "nccl":   # gloo cannot gather device tensors

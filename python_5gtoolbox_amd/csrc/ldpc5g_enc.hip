@@ -442,6 +442,15 @@ __device__ __forceinline__ void store_bits16(int8_t* dst, uint32_t b) {
                          (u >> 3) & 0x01010101u));
 }
 
+// development instrumentation (tools/enc_ts_probe.py): thread 0's real-time clock (100 MHz) at
+// phase boundaries, written over the first 64 bytes of the codeblock's output at the end
+#ifdef LDPC5G_ENC_TS
+#define ENC_TS(n) \
+    if (t == 0) enc_tsv[(n)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define ENC_TS(n)
+#endif
+
 template <bool LDSONLY>
 __device__ __forceinline__ void enc_sync() {
     if constexpr (LDSONLY) lds_sync();
@@ -453,7 +462,11 @@ __device__ __forceinline__ void enc_sync() {
 // flight across them.
 template <int BG, bool LDSONLY>
 __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_t* sm, int8_t* dst,
-                                                int Zc, int zi, int t, int NT) {
+                                                int Zc, int zi, int t, int NT
+#ifdef LDPC5G_ENC_TS
+                                                , uint64_t* enc_tsv
+#endif
+                                                ) {
     using P = BGT<BG>;
     const int K = Ly.K, W = Ly.W, DW = Ly.DW, KW = Ly.KW;
     const int S = K - 2 * Zc;
@@ -473,6 +486,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
         }
     }
     enc_sync<LDSONLY>();
+    ENC_TS(3);
 
     // ---- 3+4. lambda and the double-diagonal recursion, all inside wave 0
     constexpr int eS = (BG == 1) ? edge_of<BG>(1, 22) : edge_of<BG>(2, 10);
@@ -519,6 +533,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
         }
     }
     enc_sync<LDSONLY>();
+    ENC_TS(4);
 
     // ---- 5. extensions of the 4 core parity columns; core parity bytes straight to dn
     for (int task = t; task < 4 * DW; task += NT) {
@@ -530,6 +545,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
         store_bits(dst + S + k * Zc + 32 * w, pv[k * W + w], min(32, Zc - 32 * w));
     }
     enc_sync<LDSONLY>();
+    ENC_TS(5);
 
     // ---- 6. extension parity rows, each row-word stored straight to dn.  The row is per lane;
     //      its MAXD edge slots come from the LDS table (enc_fill_ext_tab), empty ones reading
@@ -568,6 +584,9 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     }
 }
 
+#ifndef LDPC5G_ENC_NT
+#define LDPC5G_ENC_NT 128
+#endif
 constexpr int kEncChunks = 3;   // 3 x 128 threads x 32 B >= K = 8448 (BG1 Zc=384): one round
 constexpr int kEncPieces = 6;   // 6 x 128 threads x 16 B >= K: one round (coalesced phase 1)
 template <int BG, bool LDSONLY>
@@ -578,6 +597,10 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     if (b >= B) return;
     const int t = threadIdx.x;
     const int NT = blockDim.x;
+#ifdef LDPC5G_ENC_TS
+    uint64_t enc_tsv[8] = {};
+#endif
+    ENC_TS(0);
     const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
     const int twoZ = 2 * Zc;
     extern __shared__ __align__(16) uint32_t sm[];
@@ -628,8 +651,19 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
         }
     }
     if (t < 2) sm[Ly.KW + t] = 0;
+    ENC_TS(1);
     enc_sync<LDSONLY>();
+    ENC_TS(2);
+#ifdef LDPC5G_ENC_TS
+    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT, enc_tsv);
+    ENC_TS(6);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ENC_TS(7);
+    if (t == 0) for (int q = 0; q < 8; ++q) ((uint64_t*)dst)[q] = enc_tsv[q];
+#else
     enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT);
+#endif
 }
 
 }  // namespace
@@ -642,7 +676,7 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
         // one 128-thread workgroup per codeblock (measured r01c/r01m: a pipelined persistent
         // variant 62 us, 256 threads +8 %, full barriers +0.5 % vs 25-40 us: the per-codeblock
         // LDS/VALU critical path, not HBM, sets the time, so most codeblocks in flight wins)
-        constexpr int nt = 128;
+        constexpr int nt = LDPC5G_ENC_NT;
         if (bgn == 1)
             hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
                                st, ck, dn, B, Zc, zi, ldk, ldn);

@@ -394,6 +394,11 @@ __global__ __launch_bounds__(256) void ratematch_kernel(const int8_t* __restrict
 
 // -------------------------------------------------------------------------------- receive
 constexpr int kRrNT = 512;
+// interleaver rows per thread per round in the no-repetition pass (loads in flight together;
+// r05 config 4: 1 / 2 / 4 -> 0.0621 / 0.0625 / 0.0646 ms)
+#ifndef LDPC5G_RR_RU
+#define LDPC5G_RR_RU 1
+#endif
 // the E LLRs of a codeblock are staged in LDS up to this size (4 x 512-thread workgroups per CU)
 constexpr int kRrStageBytes = 40 * 1024;
 
@@ -409,8 +414,8 @@ __device__ __forceinline__ double ld64(const Tin* p, int64_t i) { return (double
 // (lds[q*EQ + r] = llr[r*Qm + q], i.e. lds[k] is the k-th bit of the interleaver's column read-out),
 // in the same pass as the max|LLR| reduction: the input is read once, coalesced, and the gather
 // below reads LDS at consecutive k instead of global memory at stride Qm.  A row whose E is too
-// large for the stage gathers from global memory (decided per row).  Rows without repetition
-// (E <= size, the common case) take neither: see the k-major pass below.  Outputs of the gather:
+// large for the stage gathers from global memory (decided per row).  Rows visited at most twice
+// per position (E <= 2 size; the k-major passes below) take neither.  Outputs of the gather:
 // 4 consecutive positions per thread, stored as 16-B pieces when the row is 16-B aligned.
 template <typename Tin, typename Tout, bool STAGE>
 __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restrict__ llr, int64_t ldg,
@@ -436,21 +441,83 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
         return v;
     };
     double m = 0.0;
-    if (E <= s.size) {
-        // no repetition: every visited position holds exactly one LLR, (0.0 + x) / 1.  Bit k of
-        // the column read-out (k = q*EQ + r) is LLR r*Qm + q and lands at the position of rank k in
-        // the circular order from k0.  A thread per r reads its Qm consecutive LLRs (coalesced) and
-        // writes them plane by plane: consecutive r -> consecutive positions (coalesced too).
-        for (int r = threadIdx.x; r < EQ; r += kRrNT) {
-            const Tin* src = fe + (int64_t)r * s.Qm;
-            for (int q = 0; q < s.Qm; ++q) {
-                const double x = (double)src[q];
-                m = fmax(m, fabs(x));
-                int pp = q * EQ + r + s.start;   // rank + start, in the filler-free index space
-                if (pp >= s.size) pp -= s.size;
-                const int p = pp < s.f0 ? pp : pp + s.Fin;
-                orow[p] = (Tout)combine(0.0 + x, p);
+    // k-major rows: bit k of the column read-out (k = q*EQ + r) is LLR r*Qm + q and lands at the
+    // position of rank k mod size in the circular order from k0.  A thread per r reads its Qm
+    // consecutive LLRs (pairs: 8- or 16-B loads when Qm is even and the row aligned) and handles
+    // them plane by plane: consecutive r -> consecutive positions, so reads and writes coalesce.
+    // Rows visited at most twice per position (E <= 2 size) take this form when a first visit's
+    // LLR survives a round trip through the output row exactly (float input or double output):
+    // pass 1 writes every k < size — final (0.0 + x) / 1 for ranks visited once, the raw LLR for
+    // ranks visited twice — and after a barrier pass 2 combines each k >= size with it as
+    // (0.0 + x0 + x1) / 2, the reference's float64 sum of the two tmp_buf rows (:53-58).
+    const int E2 = E - s.size;   // ranks [0, E2) are visited twice
+    const bool kmaj = E <= s.size || (sizeof(Tout) >= sizeof(Tin) && E <= 2 * s.size);
+    auto pos = [&](int rank) {   // rank in [0, size) -> position in the row
+        int pp = rank + s.start;   // in the filler-free index space
+        if (pp >= s.size) pp -= s.size;
+        return pp < s.f0 ? pp : pp + s.Fin;
+    };
+    auto kmajor = [&](auto&& visit) {
+        const bool pairs = (s.Qm & 1) == 0 && ((uintptr_t)fe & (2 * sizeof(Tin) - 1)) == 0;
+        // RU interleaver rows per thread per round, all their loads in flight before any use;
+        // H = Qm / 2 pairs per row, a compile-time constant per instantiation
+        auto rounds = [&](auto hc) {
+            constexpr int H = decltype(hc)::value, RU = LDPC5G_RR_RU;
+            using V2 = Tin __attribute__((ext_vector_type(2)));
+            for (int r0 = threadIdx.x; r0 < EQ; r0 += RU * kRrNT) {
+                V2 x[RU][H];
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const int r = min(r0 + u * kRrNT, EQ - 1);   // clamped: a duplicate load, no use
+                    const V2* src = (const V2*)(fe + (int64_t)r * (2 * H));
+#pragma unroll
+                    for (int q = 0; q < H; ++q) x[u][q] = src[q];
+                }
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const int r = r0 + u * kRrNT;
+                    if (r < EQ) {
+#pragma unroll
+                        for (int q = 0; q < H; ++q)
+                            visit(2 * q * EQ + r, (double)x[u][q][0]), visit((2 * q + 1) * EQ + r, (double)x[u][q][1]);
+                    }
+                }
             }
+        };
+        if (pairs && s.Qm == 2) {
+            rounds(std::integral_constant<int, 1>{});
+        } else if (pairs && s.Qm == 4) {
+            rounds(std::integral_constant<int, 2>{});
+        } else if (pairs && s.Qm == 6) {
+            rounds(std::integral_constant<int, 3>{});
+        } else if (pairs && s.Qm == 8) {
+            rounds(std::integral_constant<int, 4>{});
+        } else if (pairs && s.Qm == 10) {
+            rounds(std::integral_constant<int, 5>{});
+        } else {
+            for (int r = threadIdx.x; r < EQ; r += kRrNT) {
+                const Tin* src = fe + (int64_t)r * s.Qm;
+                for (int q = 0; q < s.Qm; ++q) visit(q * EQ + r, (double)src[q]);
+            }
+        }
+    };
+    if (kmaj) {
+        kmajor([&](int k, double x) {
+            m = fmax(m, fabs(x));
+            if (k < s.size) {
+                const int p = pos(k);
+                orow[p] = k < E2 ? (Tout)x : (Tout)combine(0.0 + x, p);
+            }
+        });
+        if (E2 > 0) {
+            __syncthreads();   // every first visit is in the row
+            kmajor([&](int k, double x) {
+                if (k >= s.size) {
+                    const int p = pos(k - s.size);
+                    const double x0 = (double)orow[p];
+                    orow[p] = (Tout)combine((0.0 + x0 + x) / 2.0, p);
+                }
+            });
         }
     } else if (STAGE && E * (int)sizeof(Tin) <= kRrStageBytes) {   // per row: this row fits
         for (int r = threadIdx.x; r < EQ; r += kRrNT) {
@@ -474,25 +541,27 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     const double mx = m * 10.0;
     const int qE = E / s.size, rE = E - qE * s.size;   // visits of rank rr: qE + (rr < rE)
     const bool stg = STAGE && E * (int)sizeof(Tin) <= kRrStageBytes;
-    if (E <= s.size) {
-        // the positions the read-out did not reach: fillers 10 * max|LLR|, unvisited ranks and the
-        // tail past Ncb 0 (+ HARQ); disjoint from the positions written above
-        for (int p = threadIdx.x; p < s.N; p += kRrNT) {
-            double v;
-            if (p >= s.f0 && p < s.f0 + s.F) {
-                v = mx;
-            } else if (p < s.Ncb) {
-                int rr = (p < s.f0 ? p : p - s.Fin) - s.start;
-                if (rr < 0) rr += s.size;
-                if (rr < E) continue;
-                v = 0.0;
-            } else {
-                v = 0.0;
-            }
-            orow[p] = (Tout)combine(v, p);
+    if (kmaj) {
+        // the positions the read-out did not reach, disjoint from those written above: the
+        // unvisited ranks [E, size) (0; none when E > size), the fillers (10 * max|LLR|) and the
+        // tail past Ncb (0), each a range walked directly (+ HARQ)
+        for (int u = threadIdx.x; u < s.size - E; u += kRrNT) {
+            const int p = pos(E + u);
+            orow[p] = (Tout)combine(0.0, p);
         }
+        for (int p = s.f0 + (int)threadIdx.x; p < s.f0 + s.F; p += kRrNT) orow[p] = (Tout)combine(mx, p);
+        for (int p = s.Ncb + (int)threadIdx.x; p < s.N; p += kRrNT)
+            if (p < s.f0 || p >= s.f0 + s.F) orow[p] = (Tout)combine(0.0, p);
         return;
     }
+    // k -> (k mod EQ, k / EQ) without a divide: a multiply-high estimate and at most two corrections
+    const uint32_t dq = (uint32_t)EQ, mq = 0xffffffffu / dq;
+    auto divq = [&](uint32_t k, uint32_t& rem) -> uint32_t {
+        uint32_t q = __umulhi(k, mq), r = k - q * dq;
+        while (r >= dq) ++q, r -= dq;
+        rem = r;
+        return q;
+    };
     auto value = [&](int p) -> double {
         double v = 0.0;
         if (p >= s.f0 && p < s.f0 + s.F) {
@@ -505,8 +574,13 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
                 double acc = 0.0;
                 for (int j = 0; j < cnt; ++j) {
                     const int k = rr + j * s.size;
-                    if (STAGE && stg) acc += (double)lk[k];
-                    else acc += ld64(fe, (int64_t)(k % EQ) * s.Qm + k / EQ);
+                    if (STAGE && stg) {
+                        acc += (double)lk[k];
+                    } else {
+                        uint32_t kr;
+                        const uint32_t kq = divq((uint32_t)k, kr);
+                        acc += ld64(fe, (int64_t)kr * s.Qm + kq);
+                    }
                 }
                 v = cnt == 1 ? acc : acc / (double)cnt;   // x / 1.0 == x: skip the f64 divide
             }
@@ -936,6 +1010,15 @@ int64_t ldpc5g_sch_multi_plan(const ldpc5g_sch_cfg_t* cfgs, int32_t T, void* pla
     if (!plan || plan_bytes < need) return need;
     SchPlanHdr h{kSchPlanMagic, T, (int32_t)m.rows.size(), 0, m.max_E, m.dn_elems};
     for (const SchGeo& g : m.geo) h.max_cb_E = std::max(h.max_cb_E, std::max(g.s.E_lo, g.s.E_hi));
+    // rows largest first (E + N elements moved): a row is one workgroup, and a launch whose big rows
+    // come last ends on a tail of a few busy CUs (row order does not change any output)
+    std::stable_sort(m.rows.begin(), m.rows.end(), [&](const RowRef& a, const RowRef& b) {
+        auto work = [&](const RowRef& r) {
+            const SchDev& d = m.geo[r.t].s;
+            return (int64_t)(r.c < d.c_switch ? d.E_lo : d.E_hi) + d.N;
+        };
+        return work(a) > work(b);
+    });
     unsigned char* p = (unsigned char*)plan;
     memcpy(p, &h, sizeof h);
     memcpy(p + sizeof h, m.geo.data(), (size_t)gb);

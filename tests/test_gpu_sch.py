@@ -165,10 +165,15 @@ def test_raterecover_vs_reference_golden(torch, sch):
     (24000, 8, 900, 1, 2, 60000, 27000),    # E = 9000 per codeblock: f32 staged in LDS, f64 not
     (8000, 4, 700, 1, 3, 60000, 4000),      # small E: staged for both input dtypes
     (3000, 6, 300, 1, 1, 60000, 6000),      # Qm = 6 (de-interleave by 6)
+    (8000, 4, 700, 1, 3, 60000, 26000),     # E / (Ncb - F) = 1.04: two visits, k-major passes
+    (200, 2, 300, 1, 0, 60000, 2400),       # 1.80: two visits (float64 -> float32: staged gather)
+    (200, 2, 300, 1, 0, 60000, 2672),       # exactly 2.0: every rank visited twice
+    (3000, 6, 300, 1, 1, 60000, 24000),     # 1.52 with Qm = 6
 ])
 def test_raterecover_stage_paths_vs_oracle(torch, sch, args):
-    """raterecover_kernel's LDS-staged gather (E * sizeof(llr) <= 40 KB) and its global-memory
-    gather, float32 / float64 in and out, T = 3 TBs, HARQ combining: == oracle.sch_raterecover
+    """raterecover_kernel's paths — k-major passes (at most two visits per position), LDS-staged
+    gather (E * sizeof(llr) <= 40 KB), global-memory gather — float32 / float64 in and out,
+    T = 3 TBs, HARQ combining: == oracle.sch_raterecover
     (float64 bit-exact; float32 output = the float64 result rounded once)."""
     rng = np.random.default_rng(args[0])
     cfg = sch.sch_config(*args)
