@@ -929,8 +929,17 @@ def main():
             wb, eb = timed(torch, dist, world,
                            lambda: D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0), nb, 1)
             _, stb, itb = D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0)
+            line = {}
+            if algo == "BP":
+                # the per-edge messages live in a device scratch: each iteration reads and writes
+                # every edge's float64 message once (16 B per edge-update), plus the LLRs in and
+                # the decisions out once per codeblock
+                it_sum = int(itb.sum().item())
+                alg = it_sum * EDGES * 16 + Bb * (N_TX * 8 + N_FULL)
+                line = {"roofline": hbm_line(alg, eb / nb * 1e3),
+                        "edge_updates_per_s": round(it_sum * EDGES / (eb / nb), 1)}
             ex[f"{algo.lower()}_decode"] = {
-                "codeblocks_per_call": Bb, "codeblocks_per_s": round(Bb * world * nb / wb, 1),
+                "codeblocks_per_call": Bb, "codeblocks_per_s": round(Bb * world * nb / wb, 1), **line,
                 "launch_ms": round(eb / nb * 1e3, 4), "mean_iterations": round(itb.float().mean().item(), 3),
                 "note": ("hard-decision bit flipping (ldpc_decoder_bit_flipping.py:5-73)" if algo == "BF" else
                          "float64 sum-product flooding (_BP_process, nr_ldpc_decode.py:145-176), per-edge "
