@@ -573,7 +573,10 @@ __device__ __forceinline__ void dec_body(
             constexpr int d = P::RS[i + 1] - e0;
             const T mAs = getA(ic), mBs = getB(ic);
             const uint32_t pk = get_row(ic);
-            const uint32_t idxo = pk >> 24;
+            // opaque: otherwise the shift folds into an SDWA byte-select compare, which cannot take
+            // the edge index as an inline constant, and every edge pays a v_mov for it
+            uint32_t idxo = pk >> 24;
+            asm volatile("" : "+v"(idxo));
             uint32_t u = pk << (32 - d);   // bit 31 = sign of q_k for the edge k being visited
             T q[d];
             int rb[d];

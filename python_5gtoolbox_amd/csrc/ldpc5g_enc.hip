@@ -675,7 +675,9 @@ int launch_encode(const int8_t* ck, int8_t* dn, int B, int bgn, int Zc, int zi, 
     if (fast) {
         // one 128-thread workgroup per codeblock (measured r01c/r01m: a pipelined persistent
         // variant 62 us, 256 threads +8 %, full barriers +0.5 % vs 25-40 us: the per-codeblock
-        // LDS/VALU critical path, not HBM, sets the time, so most codeblocks in flight wins)
+        // LDS/VALU critical path, not HBM, sets the time, so most codeblocks in flight wins;
+        // r05: 64-thread workgroups 4.10-4.55 TB/s and two codeblocks per workgroup with the
+        // second one's loads issued before the first one's parity 4.23-4.94 TB/s, vs 4.53-5.21)
         constexpr int nt = LDPC5G_ENC_NT;
         if (bgn == 1)
             hipLaunchKernelGGL((ldpc_enc_fast_kernel<1, true>), dim3(B), dim3(nt), enc_fast_lds_bytes<1>(Zc),
