@@ -213,6 +213,33 @@ def test_mixed_plan_built_on_host():
                                            _lib.LAYERED, 0, None) == _lib.ESIZE
 
 
+def test_sch_multi_plan_rows_largest_first():
+    """ldpc5g_sch_multi_plan (pure host code): header, per-TB geometry, then one row reference
+    (TB, codeblock) per codeblock row — every row exactly once, ordered by the elements the row
+    moves (E + N) descending, so the rate-recovery launch's big rows start first."""
+    from python_5gtoolbox_amd import sch
+    cfgs = [sch.sch_config(*a) for a in ((8000, 4, 700, 1, 3, 60000, 26000), (200, 2, 300, 1, 0, 60000, 2400),
+                                          (24000, 8, 900, 1, 2, 60000, 27000), (3000, 6, 300, 1, 1, 60000, 24000))]
+    lay = sch.multi_layout(cfgs)
+    lib = _lib.lib()
+    n = lib.ldpc5g_sch_multi_plan(lay["arr"], len(cfgs), None, 0)
+    assert n > 24
+    buf = (ctypes.c_ubyte * n)()
+    assert lib.ldpc5g_sch_multi_plan(lay["arr"], len(cfgs), buf, n) == n
+    hdr = np.frombuffer(bytes(buf)[:16], np.int32)
+    nrows = sum(c.C for c in cfgs)
+    assert hdr[0] == 0x4c505253 and hdr[1] == len(cfgs) and hdr[2] == nrows
+    assert hdr[3] == max(max(c.E_lo, c.E_hi) for c in cfgs)
+    refs = np.frombuffer(bytes(buf)[n - 8 * nrows:], np.int32).reshape(nrows, 2)
+    assert sorted(map(tuple, refs.tolist())) == [(t, c) for t, cf in enumerate(cfgs) for c in range(cf.C)]
+
+    def work(t, c):
+        cf = cfgs[t]
+        return (cf.E_lo if c < cf.c_switch else cf.E_hi) + cf.N
+    w = [work(t, c) for t, c in refs]
+    assert w == sorted(w, reverse=True)
+
+
 @pytest.mark.parametrize("call,code", [
     (lambda l: l.ldpc5g_pack_records(None, 10, 2, 10, None, None, None, 1, None), _lib.ESIZE),
     (lambda l: l.ldpc5g_unpack_records(None, 8, 2, 10, None, 10, None, None, 0, None), _lib.ESIZE),
