@@ -150,6 +150,15 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bf_kernel(
 // parity with one DPP lane swap (no LDS).  The next row's messages are loaded before the current
 // row's arithmetic.  r05: 19.8 -> 10.7 ms per 1024 BG1 Zc=384 codeblocks (L=8).
 constexpr int kBpThreads = 768;   // two lanes per slot (even / odd edges of every row)
+// scheduling barrier every LDPC5G_BP_SB edges of a row (0: none) — it bounds the registers the
+// interleaved tanh / atanh chains of neighbouring edges take; LDPC5G_BP_DSADD: the row-ascending
+// LDS sums as ds_add_f64 (no return) instead of a read -> add -> write chain per edge
+#ifndef LDPC5G_BP_SB
+#define LDPC5G_BP_SB 1
+#endif
+#ifndef LDPC5G_BP_DSADD
+#define LDPC5G_BP_DSADD 1
+#endif
 constexpr double kBpClip = 2.0 * 19.07;   // (:159,161)
 constexpr int kBpMaxDeg = 19;
 
@@ -267,15 +276,22 @@ constexpr BpGroups<BG> kBpGroups{};
 // degree pads its last pair), pair slot P(i, kk) = PS[i] + kk, and a pair's two messages of slot z
 // are adjacent: msg[cb][P][z][2] -- the two lanes of a slot (even / odd edges) touch consecutive
 // 8-B words, so a wave's message loads and stores are 512 contiguous bytes.
+// Every field is 32-bit and read at a wave-uniform index, so the row loop's table reads are scalar
+// loads (the generic int8 / int16 base-graph tables compile to vector loads there, and their
+// s_waitcnt vmcnt(0) would also wait for the message prefetch in flight).
 template <int BG>
 struct BpPairs {
-    int ps[64] = {};   // first pair slot of row i
-    int np = 0;        // pair slots per codeblock
-    bool first[64] = {};   // row i starts a group of column-disjoint rows (RowGroups)
+    int ps[64] = {};      // first pair slot of row i
+    int np = 0;           // pair slots per codeblock
+    int first[64] = {};   // row i starts a group of column-disjoint rows (RowGroups)
+    int rs[64] = {};      // first edge of row i
+    int col[BGT<BG>::E] = {};   // column of edge e
     constexpr BpPairs() {
         using P = BGT<BG>;
         for (int i = 0; i < P::MB; ++i) ps[i] = np, np += (P::RS[i + 1] - P::RS[i] + 1) / 2;
-        for (int g = 0; g < kBpGroups<BG>.n; ++g) first[kBpGroups<BG>.start[g]] = true;
+        for (int g = 0; g < kBpGroups<BG>.n; ++g) first[kBpGroups<BG>.start[g]] = 1;
+        for (int i = 0; i <= P::MB; ++i) rs[i] = P::RS[i];
+        for (int e = 0; e < P::E; ++e) col[e] = P::COL[e];
     }
 };
 template <int BG>
@@ -328,10 +344,14 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
         asm volatile("" : "+v"(zo));
         return zo;
     };
+    // returned as a global (address space 1) pointer: through a generic pointer the accesses are
+    // flat_load / flat_store, which also count against lgkmcnt, so every LDS wait of the row
+    // would wait for the next row's message prefetch as well
     auto opaque_p = [&](auto* p) {
         uint64_t v = (uint64_t)(uintptr_t)p;
         asm volatile("" : "+v"(v));
-        return (decltype(p))(uintptr_t)v;
+        using E = std::remove_pointer_t<decltype(p)>;
+        return (__attribute__((address_space(1))) E*)(uintptr_t)v;
     };
     // own core column entries for the LQ update: columns j = 2jj + par_lane
     if (valid) {
@@ -346,32 +366,36 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
     __syncthreads();
 
     double pf[KK];   // r_old of the next row's own edges, loaded ahead
-    auto load_row = [&](int i, int zo, double* mr) {
-        const int d = row_start_d<BG>(i + 1) - row_start_d<BG>(i), q0 = bp_pairs_d<BG>().ps[i];
+    double pxl = 0.0;   // and the next row's extension-column LLR (rows >= 4)
+    auto load_row = [&](int i, int zo, __attribute__((address_space(1))) double* mr,
+                        const __attribute__((address_space(1))) double* lr) {
+        const int d = bp_pairs_d<BG>().rs[i + 1] - bp_pairs_d<BG>().rs[i], q0 = bp_pairs_d<BG>().ps[i];
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
             if (2 * kk < d) pf[kk] = mr[((q0 + kk) * Zc + zo) * 2 + par_lane];
+        if (i >= 4) pxl = lr[(KB + i - pc) * Zc + zo];
     };
     int it = 0;
     for (; it < L; ++it) {
         bool fail = false;
         uint64_t hdx = 0;   // ext decisions (LQ_old < 0) of the rows whose ext edge is this lane's
         if (active) {
-            load_row(0, opaque_z(), opaque_p(mrow));
+            load_row(0, opaque_z(), opaque_p(mrow), opaque_p(lrow));
             for (int i = 0; i < MB; ++i) {
                 // next row group: the LDS sums ordered.  An LDS-only barrier: __syncthreads() would
                 // also wait (vmcnt(0)) for the next row's message loads and this row's stores
                 if (bp_pairs_d<BG>().first[i] && i > 0) lds_sync();
-                const int e0 = row_start_d<BG>(i), d = row_start_d<BG>(i + 1) - e0;
+                const int e0 = bp_pairs_d<BG>().rs[i], d = bp_pairs_d<BG>().rs[i + 1] - e0;
                 const int q0 = bp_pairs_d<BG>().ps[i];
                 const int zo = opaque_z();
-                double* const mr = opaque_p(mrow);
-                const double* const lr = opaque_p(lrow);
+                const auto mr = opaque_p(mrow);
+                const auto lr = opaque_p(lrow);
                 auto rotz = [&](int sft) { int m = zo + sft; return cl * Zc + (m >= Zc ? m - Zc : m); };
                 double tq[KK];
 #pragma unroll
                 for (int kk = 0; kk < KK; ++kk) tq[kk] = pf[kk];   // r_old
-                if (i + 1 < MB) load_row(i + 1, zo, mr);
+                const double xl = pxl;
+                if (i + 1 < MB) load_row(i + 1, zo, mr, lr);
                 bool par = false;
                 int nz = 0, zk = 255;
                 double prod = 1.0, pnz = 1.0;   // product of all own t / of those with q != 0
@@ -384,9 +408,14 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                         const int k = 2 * kk + par_lane;
                         jcol[kk] = -1;
                         if (2 * kk < d) {   // wave-uniform: the pair's first edge exists
+                            // both lanes' table entries by wave-uniform (scalar) loads, then a lane
+                            // select: a lane-indexed lookup is a vector load whose s_waitcnt vmcnt(0)
+                            // would also wait for the next row's message prefetch and this row's stores
                             const int ea = e0 + 2 * kk, eb = min(ea + 1, P::E - 1);
-                            const int j = par_lane ? col_d<BG>(eb) : col_d<BG>(ea);
-                            const int sft = par_lane ? shift_of<BG>(zi, eb) : shift_of<BG>(zi, ea);
+                            const int ja = bp_pairs_d<BG>().col[ea], jb = bp_pairs_d<BG>().col[eb];
+                            const int sa = shift_of<BG>(zi, ea), sb = shift_of<BG>(zi, eb);
+                            const int j = par_lane ? jb : ja;
+                            const int sft = par_lane ? sb : sa;
                             if (k < d) {
                                 const double rold = tq[kk];
                                 double a;
@@ -394,7 +423,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                     a = app[j * kCS + rotz(sft)];
                                     jcol[kk] = j * kCS + rotz(sft);
                                 } else {
-                                    a = lr[(KB + i - pc) * Zc + zo] + rold;   // degree-1 column
+                                    a = xl + rold;   // degree-1 column
                                     hdx |= (uint64_t)(a < 0.0) << (i - 4);
                                 }
                                 par ^= a < 0.0;
@@ -410,7 +439,8 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                 }
                             }
                         }
-                        __builtin_amdgcn_sched_barrier(0);
+                        if (LDPC5G_BP_SB && kk % (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) == (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) - 1)
+                            __builtin_amdgcn_sched_barrier(0);
                     }
                 }
                 // the pair's totals (np.prod order aside: even-edge x odd-edge partial products)
@@ -436,11 +466,17 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                 } else if (nzt == 1 && k == zkt) {
                                     r = pnzt;   // prod(t[0:zk]) * prod(t[zk+1:]) (:166-172)
                                 }
-                                if (jcol[kk] >= 0) acc[jcol[kk]] += r;   // rows of a group: disjoint columns
+                                if (jcol[kk] >= 0) {   // rows of a group: disjoint columns
+                                    if (LDPC5G_BP_DSADD)
+                                        __hip_atomic_fetch_add(&acc[jcol[kk]], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    else
+                                        acc[jcol[kk]] += r;
+                                }
                             }
                             mr[((q0 + kk) * Zc + zo) * 2 + par_lane] = r;
                         }
-                        __builtin_amdgcn_sched_barrier(0);
+                        if (LDPC5G_BP_SB && kk % (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) == (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) - 1)
+                            __builtin_amdgcn_sched_barrier(0);
                     }
                 }
             }
@@ -451,7 +487,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
         hdx |= ((uint64_t)hx1 << 32) | hx0;
         if (active && flag[cl] == 0) {   // syndrome of LQ at pass start was 0 (:107-114)
             const int zo = opaque_z();
-            int8_t* const cr = opaque_p(crow);
+            const auto cr = opaque_p(crow);
             for (int j = par_lane; j < KC; j += 2) cr[j * Zc + zo] = (int8_t)(app[j * kCS + cl * Zc + zo] < 0.0);
             for (int i = 4 + par_lane; i < MB; i += 2) cr[(KB + i) * Zc + zo] = (int8_t)((hdx >> (i - 4)) & 1u);
             if (z == 0 && par_lane == 0) status[cb] = 1, iters[cb] = it;
@@ -459,7 +495,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
         }
         if (active) {   // LQ = LLRin + Lr.sum(axis=0) (:126) for the own entries; sums back to 0
             const int zo = opaque_z();
-            const double* const lr = opaque_p(lrow);
+            const auto lr = opaque_p(lrow);
             for (int j = par_lane; j < KC; j += 2) {
                 const int x = j * kCS + cl * Zc + zo;
                 const double lf = j < pc ? 0.0 : lr[(j < pc ? 0 : j - pc) * Zc + zo];
@@ -473,9 +509,9 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
     }
     // ---- exhausted: ck = LQ <= 0, status = syndrome == 0 (:133-143)
     const int zo = opaque_z();
-    double* const mr = opaque_p(mrow);
-    const double* const lr = opaque_p(lrow);
-    int8_t* const cr = opaque_p(crow);
+    const auto mr = opaque_p(mrow);
+    const auto lr = opaque_p(lrow);
+    const auto cr = opaque_p(crow);
     auto rotf = [&](int sft) { int m = zo + sft; return cl * Zc + (m >= Zc ? m - Zc : m); };
     if (active) {
         bool fail = false;

@@ -34,7 +34,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    print(f"BP B={B} snr={snr}: {ms:.3f} ms per call = {B / ms / 1e3:.1f} k CB/s, "
+    print(f"BP B={B} snr={snr}: {ms:.3f} ms per call = {B / ms:.1f} k CB/s, "
           f"mean iters {out[2].float().mean().item():.2f}, converged {int(out[1].sum().item())}", flush=True)
 
 
