@@ -660,7 +660,10 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     ENC_TS(7);
-    if (t == 0) for (int q = 0; q < 8; ++q) ((uint64_t*)dst)[q] = enc_tsv[q];
+    if (t == 0) {
+        for (int q = 0; q < 8; ++q) ((uint64_t*)dst)[q] = enc_tsv[q];
+        ((uint64_t*)dst)[8] = (uint64_t)__smid();
+    }
 #else
     enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT);
 #endif

@@ -23,7 +23,9 @@ def main():
     for _ in range(5):
         E.encode_ldpc_batch(ck, 1, out=dn)
     torch.cuda.synchronize()
-    ts = dn[:, :64].cpu().numpy().copy().view(np.int64).reshape(B, 8).astype(np.float64) / 100.0  # us
+    raw = dn[:, :72].cpu().numpy().copy().view(np.int64).reshape(B, 9)
+    ts = raw[:, :8].astype(np.float64) / 100.0  # us
+    cu = raw[:, 8]
     t0 = ts[:, 0].min()
     ts -= t0
     names = ["loads+pack", "sync1", "X ext", "recursion", "core parity", "ext rows", "drain"]
@@ -32,6 +34,18 @@ def main():
           f"(p10 {np.percentile(ts[:, 7] - ts[:, 0], 10):.2f}, p90 {np.percentile(ts[:, 7] - ts[:, 0], 90):.2f})")
     for i, n in enumerate(names):
         print(f"  {n:>12}: mean {d[:, i].mean():6.2f} us  p90 {np.percentile(d[:, i], 90):6.2f}")
+    # most workgroups resident together on one CU (by __smid), over the launch
+    t0s, t1s = ts[:, 0] - ts[:, 0].min(), ts[:, 7] - ts[:, 0].min()
+    peak = []
+    for c in np.unique(cu):
+        m = cu == c
+        ev = sorted([(a, 1) for a in t0s[m]] + [(b, -1) for b in t1s[m]], key=lambda x: (x[0], x[1]))
+        cur = best = 0
+        for _, d in ev:
+            cur += d
+            best = max(best, cur)
+        peak.append(best)
+    print(f"  CUs seen {len(peak)}, resident workgroups per CU: max {max(peak)}, median {int(np.median(peak))}, min {min(peak)}")
     for q in (0.1, 0.25, 0.5, 0.75, 0.9, 1.0):
         t = ts[:, 7].max() * q
         live = np.sum((ts[:, 0] <= t) & (ts[:, 7] >= t))
