@@ -462,7 +462,7 @@ __device__ __forceinline__ void enc_sync() {
 // flight across them.
 template <int BG, bool LDSONLY>
 __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_t* sm, int8_t* dst,
-                                                int Zc, int zi, int t, int NT
+                                                int Zc, int zi, int t, int NT, bool direct
 #ifdef LDPC5G_ENC_TS
                                                 , uint64_t* enc_tsv
 #endif
@@ -475,8 +475,9 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
     uint32_t* lam = X + P::KC * DW;
     uint32_t* pv = lam + 4 * W;   // p1 p2 p3 p4 L2
 
-    // ---- 2. periodic extensions of the information columns (task = j * DW + q)
-    {
+    // ---- 2. periodic extensions of the information columns (task = j * DW + q); skipped when
+    //      phase 1 already wrote them (Zc % 32 == 0, coalesced path: enc_direct_x)
+    if (!direct) {
         const int dj = NT / DW, dq = NT - dj * DW;
         int j = t / DW, q = t - j * DW;
         for (int task = t; task < P::KB * DW; task += NT) {
@@ -485,7 +486,7 @@ __device__ __forceinline__ void enc_fast_parity(const EncFastLayout& Ly, uint32_
             if (q >= DW) q -= DW, ++j;
         }
     }
-    enc_sync<LDSONLY>();
+    if (!direct) enc_sync<LDSONLY>();
     ENC_TS(3);
 
     // ---- 3+4. lambda and the double-diagonal recursion, all inside wave 0
@@ -603,6 +604,10 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     ENC_TS(0);
     const EncFastLayout Ly = enc_fast_layout<BG>(Zc);
     const int twoZ = 2 * Zc;
+    // Zc % 32 == 0 on the coalesced path: phase 1 writes the periodic extensions itself (no
+    // phase 2 and one barrier less); w / W by a multiply-high (exact: w < 2^10, 2 <= W <= 12)
+    const bool direct = (Zc & 31) == 0 && (NT & 63) == 0;
+    const uint32_t wdiv = (uint32_t)(0xffffffffu / (uint32_t)Ly.W) + 1u;
     extern __shared__ __align__(16) uint32_t sm[];
     const int8_t* src = ck + (int64_t)b * ldk;
     int8_t* dst = dn + (int64_t)b * ldn;
@@ -629,7 +634,19 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
                 if (pc - (t & 63) >= np) break;   // wave-uniform
                 uint32_t part = pc < np ? enc_pack_half(v[c], 16 * pc, pc & 1, twoZ, dst) : 0u;
                 part |= (uint32_t)__shfl_xor((int)part, 1, 64);
-                if (pc < np && !(pc & 1)) sm[pc >> 1] = part;
+                if (pc < np && !(pc & 1)) {
+                    const int w = pc >> 1;
+                    if (direct) {
+                        // word q of column j straight into its periodic extension X_j (word
+                        // copies: X_j[q] = X_j[W + q] = block_j[q], and the two words past 2W)
+                        const int j = Ly.W == 1 ? w : (int)__umulhi((uint32_t)w, wdiv), q = w - j * Ly.W;
+                        uint32_t* xj = sm + Ly.KW + 2 + j * Ly.DW;
+                        xj[q] = part, xj[Ly.W + q] = part;
+                        if (q < 2) xj[2 * Ly.W + q] = part;
+                    } else {
+                        sm[w] = part;
+                    }
+                }
             }
         }
     } else
@@ -655,7 +672,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
     enc_sync<LDSONLY>();
     ENC_TS(2);
 #ifdef LDPC5G_ENC_TS
-    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT, enc_tsv);
+    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT, direct, enc_tsv);
     ENC_TS(6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -665,7 +682,7 @@ __global__ __launch_bounds__(256) void ldpc_enc_fast_kernel(const int8_t* __rest
         ((uint64_t*)dst)[8] = (uint64_t)__smid();
     }
 #else
-    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT);
+    enc_fast_parity<BG, LDSONLY>(Ly, sm, dst, Zc, zi, t, NT, direct);
 #endif
 }
 
