@@ -141,12 +141,14 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
     std::vector<DecWork> work[2];
     std::vector<CbRef> refs;
     int nz1 = 0;
-    // workgroups heaviest first (lifting sizes descending, full workgroups before a bucket's
-    // partial one): the dispatcher hands them to CUs in list order, so the light ones fill the
-    // gaps at the end instead of a few heavy ones forming the tail (r05 config 4: ascending order
-    // left 1.04 ms).  BG1's full Zc = 384 workgroups are then the head of its list.
+    // lifting sizes ascending: the dispatcher hands workgroups to CUs in list order, and the
+    // longest-running ones come first — a small-Zc workgroup holds G = 768 / Zc codeblocks (64 at
+    // Zc = 12) and runs until its slowest one stops, nearly always all L iterations, while a
+    // Zc = 384 workgroup (2 codeblocks) often exits early (r05 config 4: 0.951 ms per decode vs
+    // 0.965 with lifting sizes descending).  Per bucket a partial workgroup first, then the full
+    // ones: BG1's full Zc = 384 workgroups are the tail of its list (their own kernel, see below).
     for (int g = 0; g < 2; ++g)
-        for (int zi = LDPC5G_NUM_ZC - 1; zi >= 0; --zi) {
+        for (int zi = 0; zi < LDPC5G_NUM_ZC; ++zi) {
             const std::vector<int>& v = bucket[g][zi];
             const int Zc = kLdpcZcList[zi], G = dec_G(Zc, schedule == LDPC5G_LAYERED);
             const size_t part = v.size() % G;
@@ -160,8 +162,8 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
                 }
                 work[g].push_back(w);
             };
-            for (size_t s = part; s < v.size(); s += G) emit(s, G);
             if (part) emit(0, (int)part);
+            for (size_t s = part; s < v.size(); s += G) emit(s, G);
             if (g == 0 && Zc == 384) nz1 = (int)((v.size() - part) / G);
         }
     const int64_t need = (int64_t)sizeof(MixedPlanHdr) + (int64_t)(work[0].size() + work[1].size()) * (int64_t)sizeof(DecWork) +
@@ -211,7 +213,7 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     const DecWork* w2 = w1 + h.nw1;
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
     const bool lay = h.schedule == LDPC5G_LAYERED;
-    // BG1's full Zc = 384 work items (the head of its list) run the Zc = 384 kernels of mixed plans
+    // BG1's full Zc = 384 work items (the tail of its list) run the Zc = 384 kernels of mixed plans
     // (layered float32, flooding float64; a mixed plan's float32 flooding items and BG2 items keep the
     // generic kernels, although launch_flood_t has Zc = 384 kernels for those too) — as their own launch, so only when they fill the GPU on
     // their own (>= 2 workgroups per CU of the MI355X's 256): a smaller set stays in the shared
@@ -229,13 +231,13 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     for (int g = 0; g < 2; ++g) {
         const int nwg = g == 0 ? h.nw1 - nz : h.nw2;
         hipStream_t sg = g == 1 && side ? side->s : st;
-        if (g == 0 && nz > 0)
-            if (int rc = launch_dec_mixed(1, llr_dtype, lay, llr_base, ck_base, status, iters, nz, w1, r, L,
-                                          alpha, beta, pc, dead, st, true))
-                return rc;
         if (nwg > 0)
             if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
-                                          g == 0 ? w1 + nz : w2, r, L, alpha, beta, pc, dead, sg))
+                                          g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, sg))
+                return rc;
+        if (g == 0 && nz > 0)
+            if (int rc = launch_dec_mixed(1, llr_dtype, lay, llr_base, ck_base, status, iters, nz,
+                                          w1 + (h.nw1 - nz), r, L, alpha, beta, pc, dead, st, true))
                 return rc;
     }
     if (side) {

@@ -19,8 +19,11 @@
 // behind which one lane adds to the counter, the counter is polled with an `sc1` load and every load
 // of hand-off data is an `sc1` global load (MI355X_MICROARCH.md, hand-off table first row): no L2
 // write-back or L1 invalidate fence on the critical path.  All W*B workgroups must be resident
-// together: the launcher keeps B*W <= kSplitMaxWG (half the CUs) and one workgroup per CU.
+// together: the launcher keeps B*W <= kSplitMaxWG (half the CUs), one workgroup per CU, and chains
+// the split launches of a device one after another across streams (an event per device).
 #include <stdlib.h>
+
+#include <mutex>
 
 #include "ldpc5g_dec_small.h"
 
@@ -370,10 +373,23 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
     uint32_t* sync = (uint32_t*)((char*)p + data);
     int rc = check_hip(hipMemsetAsync(sync, 0, (size_t)B * kSplitSync * 4, st), "hipMemsetAsync");
     if (!rc) {
-        auto kern = beta != 0.0 ? ldpc_split_kernel<BG, true> : ldpc_split_kernel<BG, false>;
-        hipLaunchKernelGGL(kern, dim3(B * W), dim3(kSplitThreads), 0, st, llr, ck, status, iters, Zc, zi, W,
-                           ldl, ldc, L, alpha, beta, pc, (double*)p, sync);
-        rc = check_hip(hipGetLastError(), "ldpc_split_kernel launch");
+        // split launches of one device run one after another, whatever their streams: each needs
+        // all of its <= kSplitMaxWG workgroups resident together, and two or more launches sharing
+        // the CUs could each hold part of the chip while waiting for the rest (their barriers would
+        // never complete).  A per-device event chain orders them; on one stream it costs nothing.
+        static std::mutex mu;
+        static hipEvent_t last[64] = {};
+        std::lock_guard<std::mutex> lk(mu);
+        hipEvent_t& ev = last[dev & 63];
+        if (!ev) rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate (split chain)");
+        else rc = check_hip(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent (split chain)");
+        if (!rc) {
+            auto kern = beta != 0.0 ? ldpc_split_kernel<BG, true> : ldpc_split_kernel<BG, false>;
+            hipLaunchKernelGGL(kern, dim3(B * W), dim3(kSplitThreads), 0, st, llr, ck, status, iters, Zc, zi, W,
+                               ldl, ldc, L, alpha, beta, pc, (double*)p, sync);
+            rc = check_hip(hipGetLastError(), "ldpc_split_kernel launch");
+            if (!rc) rc = check_hip(hipEventRecord(ev, st), "hipEventRecord (split chain)");
+        }
     }
     const int rf = check_hip(hipFreeAsync(p, st), "hipFreeAsync");
     return rc ? rc : rf;

@@ -271,6 +271,32 @@ def test_decode_split_kernel_vs_oracle(torch, dec, bg, Zc, B):
                 assert np.array_equal(g, r), (L, alpha, beta, rm)
 
 
+def test_decode_split_kernel_concurrent_streams(torch, dec):
+    """Three streams each launching the multi-workgroup kernel with 7 BG1 Zc=384 codeblocks (126
+    workgroups each, 378 together: more than the CUs hold at once) — the library chains split
+    launches of a device one after another, so none can wait forever for CUs the others hold;
+    results equal a sequential run."""
+    rng = np.random.default_rng(77)
+    Zc, B = 384, 7
+    xs = []
+    for s_ in range(3):
+        ck = rng.integers(0, 2, (B, 22 * Zc)).astype(np.int8)
+        dn = O.encode(ck, 1)
+        llr = 2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (3 / 20)) / 10 ** (3 / 10)
+        xs.append(torch.from_numpy(llr).cuda())
+    ref = [[t.cpu() for t in dec.nr_decode_ldpc_batch(x, Zc, 1, 8, "min-sum", 0.75, 0.0, "flooding")] for x in xs]
+    streams = [torch.cuda.Stream() for _ in xs]
+    outs = []
+    torch.cuda.synchronize()
+    for st, x in zip(streams, xs):
+        with torch.cuda.stream(st):
+            outs.append(dec.nr_decode_ldpc_batch(x, Zc, 1, 8, "min-sum", 0.75, 0.0, "flooding"))
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        for a, b in zip(o, r):
+            assert torch.equal(a.cpu(), b)
+
+
 def test_decode_ldpc_full_length(torch, dec):
     """decode_ldpc(LLRin, H, ...) — full-length LLR incl. the punctured columns — matches the
     oracle fed the same full row."""

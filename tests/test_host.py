@@ -202,11 +202,11 @@ def test_mixed_plan_built_on_host():
         assert lib.ldpc5g_mixed_plan(d, 8, sched, buf, n) == n
         hdr = np.frombuffer(bytes(buf)[:24], np.int32)
         assert hdr[1] == sched and hdr[2] == nw1 and hdr[3] == nw2 and hdr[4] == 8
-        # the BG1 Zc=384 items: the nz1 full workgroups first (heaviest first; the Zc = 384
-        # kernels' share when split off), then the partial one
+        # the BG1 Zc=384 items: a partial workgroup first, then the nz1 full ones (the Zc = 384
+        # kernels' share, launched last)
         assert hdr[5] == nz1
         work = np.frombuffer(bytes(buf)[24:24 + 16 * nw1], np.int32).reshape(nw1, 4)
-        assert list(work[:, 2]) == ([2, 2, 1] if sched == _lib.LAYERED else [1] * 5)
+        assert list(work[:, 2]) == ([1, 2, 2] if sched == _lib.LAYERED else [1] * 5)
     d[3].Zc = 383
     assert lib.ldpc5g_mixed_plan(d, 8, _lib.LAYERED, None, 0) == _lib.EZC
     assert lib.ldpc5g_decode_ms_mixed_plan(None, None, None, 1, None, None, None, 8, 1.0, 0.0,
