@@ -64,8 +64,9 @@ def pmc_entry(kernel):
     kernel reports None until its counters are collected again)."""
     try:
         with open(PMC_SUMMARY) as f:
-            return json.load(f)["kernels"][kernel]
-    except (OSError, KeyError, ValueError):
+            d = json.load(f)
+        return d.get("kernels", d)[kernel]   # (a bare per-kernel dict is accepted too)
+    except (OSError, KeyError, ValueError, AttributeError):
         return None
 
 

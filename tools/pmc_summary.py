@@ -45,7 +45,9 @@ def main(d):
             e["hbm_bytes_raw"] = (e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
             e["hbm_bytes_fetch16_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
         out[k] = e
-    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    # the format bench.py reads (profiles/pmc_latest.json): {"source": ..., "kernels": {name: ...}}
+    json.dump({"source": f"{d} (tools/gpu_round.sh pmc passes -> tools/pmc_summary.py)", "kernels": out},
+              sys.stdout, indent=1, sort_keys=True)
     print()
 
 
