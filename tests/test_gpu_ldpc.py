@@ -312,6 +312,24 @@ def test_decode_ldpc_full_length(torch, dec):
         assert np.array_equal(ck, ock) and st == ost
 
 
+@pytest.mark.parametrize("bg,Zc", [(1, 384), (2, 96), (1, 120)])
+def test_decode_split_kernel_full_length(torch, dec, bg, Zc):
+    """decode_ldpc with a full-length LLR row (the punctured columns carry LLRs: pc = 0) through
+    the multi-workgroup kernel (one large codeblock per call) == the oracle on the same row."""
+    from python_5gtoolbox_amd import ldpc_info
+    rng = np.random.default_rng(Zc + bg)
+    K = (22 if bg == 1 else 10) * Zc
+    ck0 = rng.integers(0, 2, (1, K)).astype(np.int8)
+    dn = O.encode(ck0, bg)[0]
+    full = np.concatenate([1 - 2 * ck0[0, :2 * Zc].astype(np.float64), 1 - 2 * dn.astype(np.float64)])
+    full = 2 * (full + rng.normal(size=full.shape) * 0.9) / 0.81
+    H = ldpc_info.getH(Zc, bg, ldpc_info.find_iLS(Zc))
+    for L, a, b in ((8, 0.75, 0.0), (5, 1.0, 0.3)):
+        ck, st = dec.decode_ldpc(full, H, L, "min-sum", a, b)
+        ock, ost = _oracle_full(full, Zc, bg, L, a, b)
+        assert np.array_equal(ck, ock) and st == ost, (L, a, b)
+
+
 def _oracle_full(full, Zc, bg, L, a, b):
     """Flooding restatement with caller-provided LLRs on every column (decode_ldpc semantics)."""
     g = O.graph(bg, Zc)
