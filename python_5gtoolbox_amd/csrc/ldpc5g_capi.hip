@@ -186,8 +186,8 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
 // round of workgroups).  Ordered against the caller's stream by two events; created once, never
 // destroyed (like the staging buffers).
 struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t s = nullptr, s2 = nullptr;   // s2: the Zc = 384 share of a mixed plan (LDPC5G_MIX_Z3)
+    hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
 };
 thread_local SideStream t_side[64];
 
@@ -200,12 +200,20 @@ int side_stream(SideStream** out) {
         if (int rc = check_hip(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking), "hipStreamCreate(side)")) return rc;
         if (int rc = check_hip(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming), "hipEventCreate(fork)")) return rc;
         if (int rc = check_hip(hipEventCreateWithFlags(&x.join, hipEventDisableTiming), "hipEventCreate(join)")) return rc;
+        if (int rc = check_hip(hipStreamCreateWithFlags(&x.s2, hipStreamNonBlocking), "hipStreamCreate(side 2)")) return rc;
+        if (int rc = check_hip(hipEventCreateWithFlags(&x.join2, hipEventDisableTiming), "hipEventCreate(join2)")) return rc;
     }
     *out = &x;
     return LDPC5G_OK;
 }
 
 // launches of a plan (host copy `h` for the counts, device copy `dev` for the kernels)
+// BG1's full Zc = 384 work items on a third stream with the Zc = 384 kernel, however few (r05
+// config 4: 171 of them, step 1.017 -> 1.004 ms, decode 0.938 -> 0.930); 0: only when >= 512 of
+// them, in line on the caller's stream
+#ifndef LDPC5G_MIX_Z3
+#define LDPC5G_MIX_Z3 1
+#endif
 int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr_base, int llr_dtype,
                 int8_t* ck_base, uint8_t* status, int32_t* iters, int L, double alpha, double beta,
                 int pc, bool dead, hipStream_t st) {
@@ -214,16 +222,17 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
     const bool lay = h.schedule == LDPC5G_LAYERED;
     // BG1's full Zc = 384 work items (the tail of its list) run the Zc = 384 kernels of mixed plans
-    // (layered float32, flooding float64; a mixed plan's float32 flooding items and BG2 items keep the
-    // generic kernels, although launch_flood_t has Zc = 384 kernels for those too) — as their own launch, so only when they fill the GPU on
-    // their own (>= 2 workgroups per CU of the MI355X's 256): a smaller set stays in the shared
-    // launch, where it overlaps the other lifting sizes (config 4's 171 workgroups measured 1.04 ->
-    // 1.17 ms split off)
-    constexpr int kZcSplitMin = 512;
+    // (layered float32, flooding float64; a mixed plan's float32 flooding items and BG2 items keep
+    // the generic kernels, although launch_flood_t has Zc = 384 kernels for those too) as their own
+    // launch on a third stream beside the rest (LDPC5G_MIX_Z3; in line on the caller's stream they
+    // paid only when they fill the GPU on their own: config 4's 171 workgroups measured 1.04 ->
+    // 1.17 ms split off in line)
+    constexpr int kZcSplitMin = LDPC5G_MIX_Z3 ? 1 : 512;
     const int nz = (lay || llr_dtype == LDPC5G_F64) && h.nz1 >= kZcSplitMin ? std::min(h.nz1, h.nw1) : 0;
     // BG2 on the side stream when both base graphs are present (forked from / joined into st)
     SideStream* side = nullptr;
-    if (h.nw2 > 0 && h.nw1 > 0) {
+    const bool z3 = LDPC5G_MIX_Z3 && nz > 0 && h.nw1 - nz > 0;   // the Zc = 384 share on a third stream
+    if ((h.nw2 > 0 && h.nw1 > 0) || z3) {
         if (int rc = side_stream(&side)) return rc;
         if (int rc = check_hip(hipEventRecord(side->fork, st), "hipEventRecord(fork)")) return rc;
         if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "hipStreamWaitEvent(fork)")) return rc;
@@ -235,12 +244,20 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
             if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
                                           g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, sg))
                 return rc;
-        if (g == 0 && nz > 0)
+        if (g == 0 && nz > 0) {
+            hipStream_t sz = z3 ? side->s2 : st;
+            if (z3)
+                if (int rc = check_hip(hipStreamWaitEvent(sz, side->fork, 0), "hipStreamWaitEvent(fork 2)")) return rc;
             if (int rc = launch_dec_mixed(1, llr_dtype, lay, llr_base, ck_base, status, iters, nz,
-                                          w1 + (h.nw1 - nz), r, L, alpha, beta, pc, dead, st, true))
+                                          w1 + (h.nw1 - nz), r, L, alpha, beta, pc, dead, sz, true))
                 return rc;
+            if (z3) {
+                if (int rc = check_hip(hipEventRecord(side->join2, sz), "hipEventRecord(join2)")) return rc;
+                if (int rc = check_hip(hipStreamWaitEvent(st, side->join2, 0), "hipStreamWaitEvent(join2)")) return rc;
+            }
+        }
     }
-    if (side) {
+    if (side && h.nw2 > 0) {
         if (int rc = check_hip(hipEventRecord(side->join, side->s), "hipEventRecord(join)")) return rc;
         if (int rc = check_hip(hipStreamWaitEvent(st, side->join, 0), "hipStreamWaitEvent(join)")) return rc;
     }
