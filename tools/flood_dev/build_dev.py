@@ -50,6 +50,9 @@ FLAGS = {
     "pre2sb": ["-DLDPC5G_FLOOD_APRE=2", "-DLDPC5G_FLOOD_ASB=1"],
     "pre3sb": ["-DLDPC5G_FLOOD_APRE=3", "-DLDPC5G_FLOOD_ASB=1"],
     "nosxpop": ["-DLDPC5G_FLOOD_SXPOP=0"],
+    "x2": ["-DLDPC5G_FLOOD_XPRE=2"],
+    "x6": ["-DLDPC5G_FLOOD_XPRE=6"],
+    "x8": ["-DLDPC5G_FLOOD_XPRE=8"],
 }
 for _n in FLAGS:
     VARIANTS.setdefault(_n, [])
