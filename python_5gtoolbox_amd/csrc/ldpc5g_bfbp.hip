@@ -150,15 +150,16 @@ __global__ __launch_bounds__(kBfThreads) void ldpc_bf_kernel(
 // parity with one DPP lane swap (no LDS).  The next row's messages are loaded before the current
 // row's arithmetic.  r05: 19.8 -> 10.7 ms per 1024 BG1 Zc=384 codeblocks (L=8).
 constexpr int kBpThreads = 768;   // two lanes per slot (even / odd edges of every row)
-// scheduling barrier every LDPC5G_BP_SB edges of a row (0: none) — it bounds the registers the
-// interleaved tanh / atanh chains of neighbouring edges take; LDPC5G_BP_DSADD: the row-ascending
-// LDS sums as ds_add_f64 (no return) instead of a read -> add -> write chain per edge
+// scheduling barrier every LDPC5G_BP_SB edges of a row (0: none): it bounds the registers the
+// interleaved tanh / atanh chains of neighbouring edges take (r05: 1 / 2 / 0 measured 8.60 / 8.60
+// / 8.65 ms per 1024 BG1 Zc=384 codeblocks)
 #ifndef LDPC5G_BP_SB
 #define LDPC5G_BP_SB 1
 #endif
-#ifndef LDPC5G_BP_DSADD
-#define LDPC5G_BP_DSADD 1
-#endif
+constexpr int kBpSb = LDPC5G_BP_SB;
+__device__ __forceinline__ void bp_sched_point(int kk) {
+    if (kBpSb > 0 && kk % (kBpSb > 0 ? kBpSb : 1) == (kBpSb > 0 ? kBpSb : 1) - 1) __builtin_amdgcn_sched_barrier(0);
+}
 constexpr double kBpClip = 2.0 * 19.07;   // (:159,161)
 constexpr int kBpMaxDeg = 19;
 
@@ -439,8 +440,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                 }
                             }
                         }
-                        if (LDPC5G_BP_SB && kk % (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) == (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) - 1)
-                            __builtin_amdgcn_sched_barrier(0);
+                        bp_sched_point(kk);
                     }
                 }
                 // the pair's totals (np.prod order aside: even-edge x odd-edge partial products)
@@ -466,17 +466,14 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                 } else if (nzt == 1 && k == zkt) {
                                     r = pnzt;   // prod(t[0:zk]) * prod(t[zk+1:]) (:166-172)
                                 }
-                                if (jcol[kk] >= 0) {   // rows of a group: disjoint columns
-                                    if (LDPC5G_BP_DSADD)
-                                        __hip_atomic_fetch_add(&acc[jcol[kk]], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                    else
-                                        acc[jcol[kk]] += r;
-                                }
+                                // rows of a group: disjoint columns; ds_add_f64 (no return), not a
+                                // read -> add -> write chain (r05: 8.98 -> 8.90 ms)
+                                if (jcol[kk] >= 0)
+                                    __hip_atomic_fetch_add(&acc[jcol[kk]], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             }
                             mr[((q0 + kk) * Zc + zo) * 2 + par_lane] = r;
                         }
-                        if (LDPC5G_BP_SB && kk % (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) == (LDPC5G_BP_SB ? LDPC5G_BP_SB : 1) - 1)
-                            __builtin_amdgcn_sched_barrier(0);
+                        bp_sched_point(kk);
                     }
                 }
             }
