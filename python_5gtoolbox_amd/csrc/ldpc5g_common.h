@@ -180,9 +180,9 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
                      const CbRef* cbs, int L, double alpha, double beta, int pc, bool dead,
                      hipStream_t st, bool zc384 = false);
 // float64 flooding of a few large codeblocks, each over W = split_parts workgroups
-// (ldpc5g_dec_split.hip); split_wanted: the launch shape it serves (B * W <= half the CUs)
-int split_parts(int bgn, int Zc);
-bool split_wanted(int bgn, int B, int Zc);
+// (ldpc5g_dec_split.hip); split_wanted: the chunks per wave R (1 or 2) of a launch it serves, or 0
+int split_parts(int bgn, int Zc, int R);
+int split_wanted(int bgn, int B, int Zc);
 int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
                        int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta,
                        int pc, hipStream_t st);

@@ -19,8 +19,9 @@
 // behind which one lane adds to the counter, the counter is polled with an `sc1` load and every load
 // of hand-off data is an `sc1` global load (MI355X_MICROARCH.md, hand-off table first row): no L2
 // write-back or L1 invalidate fence on the critical path.  All W*B workgroups must be resident
-// together: the launcher keeps B*W <= kSplitMaxWG (half the CUs), one workgroup per CU, and chains
-// the split launches of a device one after another across streams (an event per device).
+// together: the launcher keeps B*W <= kSplitMaxWG (224 of the 256 CUs), one workgroup per CU, and
+// chains the split launches of a device one after another across streams (an event per device).
+// Launches of more codeblocks take R = 2 chunks per wave (half the workgroups per codeblock).
 #include <stdlib.h>
 
 #include <mutex>
@@ -32,7 +33,7 @@ namespace {
 
 constexpr int kSplitThreads = 1024;
 constexpr int kSplitSync = 64;   // sync words per codeblock (a 256-B line): barrier counter, flags
-constexpr int kSplitMaxWG = 128;
+constexpr int kSplitMaxWG = 224;   // of the 256 CUs, one workgroup each
 // loads in flight per chunk (phase A LQ reads, phase B message reads); 32: a row's / column's all
 // at once (r05, one BG1 Zc=384 codeblock: 10 / 10 100 us per call, all 87 us)
 #ifndef LDPC5G_SPLIT_CH
@@ -100,7 +101,10 @@ struct SplitPlan {
 template <int BG>
 __device__ constexpr SplitPlan<BG> kSplitPlanD{};
 
-template <int BG, bool OFS>
+// R chunks per wave (R = 2 halves the workgroups per codeblock, so twice as many codeblocks fit
+// one launch): wave v of workgroup w owns chunks of rounds v*R .. v*R + R-1, each round dealt
+// snake-wise as above; the chunks of a wave are walked one after the other in each phase.
+template <int BG, bool OFS, int R>
 __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int Zc, int zi, int W, int64_t ldl, int64_t ldc, int L, double alpha,
@@ -109,7 +113,8 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     using T = double;
     constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = 8;
     constexpr int DMAX = kSmallPlanH<BG>.dmax, CMAX = kSmallPlanH<BG>.cmax;
-    constexpr int CH = LDPC5G_SPLIT_CH, CCH = LDPC5G_SPLIT_CCH;   // loads in flight per chunk: phase A, B
+    // loads in flight per chunk (phase A, B); R = 2 keeps twice the chunk state, so fewer
+    constexpr int CH = R == 1 ? LDPC5G_SPLIT_CH : 16, CCH = R == 1 ? LDPC5G_SPLIT_CCH : 16;
     __shared__ uint32_t rws[MB * DMAX], wws[MB * DMAX];   // edge words per (row, edge < DMAX)
     __shared__ uint32_t lfail, lflag;
 
@@ -163,143 +168,163 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     }
     if (t == 0) lfail = 0u;
     const int nch = (Zc + 63) >> 6;   // chunks per row / column
-    const int ch = v * W + ((v & 1) ? W - 1 - w : w);   // this wave's chunk (rank in degree order)
-    // own core column entry (cj, cz): LLR, CSC range (column-uniform: SGPRs)
-    const bool hasc_w = ch < KC * nch;
-    const int cj = hasc_w ? kSplitPlanD<BG>.cord[ch / nch] : 0;
-    const int cz = (ch % nch) * 64 + lane;
-    const bool hasc = hasc_w && cz < Zc;
-    const int cn = kSmallPlanD<BG>.cstart[cj + 1] - kSmallPlanD<BG>.cstart[cj];
-    const uint32_t cr0 = (uint32_t)kSmallPlanD<BG>.cstart[cj] * ZT + (uint32_t)cz * TS;
-    const uint32_t cq = (uint32_t)cj * ZT + (uint32_t)cz * TS;   // LQ entry
-    const bool cpun = cj < pc;
-    const T lf = (hasc && !cpun) ? lrow[(cj - pc) * Zc + cz] : T(0);
-    T lqv = lf;
-    if (hasc) st_sc1(lq, cq, lf);
-    // own check node (ri, rz): row state (nA, nB, signs | argmin << 24), extension LLR
-    const bool hasn_w = ch < MB * nch;
-    const int ri = hasn_w ? kSplitPlanD<BG>.rord[ch / nch] : 0;
-    const int rz = (ch % nch) * 64 + lane;
-    const bool hasn = hasn_w && rz < Zc;
-    const uint32_t zb0 = (uint32_t)rz * TS, re0 = (uint32_t)(ri * DMAX);
-    const int rd = row_start_d<BG>(ri + 1) - row_start_d<BG>(ri);
-    const bool xe = ri >= 4;   // rows >= 4: the last edge is the extension column
-    const int dc = rd - (xe ? 1 : 0);
-    const T xl = (hasn && xe) ? lrow[(KB + ri - pc) * Zc + rz] : T(0);
-    T nA = T(0), nB = T(0);
-    uint32_t wd = 0u;
+    // per chunk slot k < R: own core column entry (cj, cz) and own check node (ri, rz)
+    int cj[R], cn[R], ri[R], rd[R], dc[R], cz[R], rz[R];
+    uint32_t cr0[R], cq[R], zb0[R], re0[R], wd[R];
+    bool hasc[R], cpun[R], hasn[R], xe[R], hdx[R];
+    T lf[R], lqv[R], xl[R], nA[R], nB[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int round = v * R + k;
+        const int ch = round * W + ((round & 1) ? W - 1 - w : w);   // chunk (rank in degree order)
+        const bool hasc_w = ch < KC * nch;
+        cj[k] = hasc_w ? kSplitPlanD<BG>.cord[ch / nch] : 0;
+        cz[k] = (ch % nch) * 64 + lane;
+        hasc[k] = hasc_w && cz[k] < Zc;
+        cn[k] = kSmallPlanD<BG>.cstart[cj[k] + 1] - kSmallPlanD<BG>.cstart[cj[k]];
+        cr0[k] = (uint32_t)kSmallPlanD<BG>.cstart[cj[k]] * ZT + (uint32_t)cz[k] * TS;
+        cq[k] = (uint32_t)cj[k] * ZT + (uint32_t)cz[k] * TS;   // LQ entry
+        cpun[k] = cj[k] < pc;
+        lf[k] = (hasc[k] && !cpun[k]) ? lrow[(cj[k] - pc) * Zc + cz[k]] : T(0);
+        lqv[k] = lf[k];
+        if (hasc[k]) st_sc1(lq, cq[k], lf[k]);
+        const bool hasn_w = ch < MB * nch;
+        ri[k] = hasn_w ? kSplitPlanD<BG>.rord[ch / nch] : 0;
+        rz[k] = (ch % nch) * 64 + lane;
+        hasn[k] = hasn_w && rz[k] < Zc;
+        zb0[k] = (uint32_t)rz[k] * TS, re0[k] = (uint32_t)(ri[k] * DMAX);
+        rd[k] = row_start_d<BG>(ri[k] + 1) - row_start_d<BG>(ri[k]);
+        xe[k] = ri[k] >= 4;   // rows >= 4: the last edge is the extension column
+        dc[k] = rd[k] - (xe[k] ? 1 : 0);
+        xl[k] = (hasn[k] && xe[k]) ? lrow[(KB + ri[k] - pc) * Zc + rz[k]] : T(0);
+        nA[k] = T(0), nB[k] = T(0), wd[k] = 0u, hdx[k] = false;
+    }
     uint32_t mv = 0x80000000u;
     asm volatile("" : "+v"(mv));
     grid_sync(1, 0u);
     SPLIT_TS(1);
 
-    bool hdx = false;
     int it = 0;
     for (; it < L; ++it) {
-        // ---- phase A (rows from LQ_old, syndrome of LQ_old): the wave's row, its dc core edges
+        // ---- phase A (rows from LQ_old, syndrome of LQ_old): each chunk's row, its dc core edges
         bool fail = false;
-        // per-iteration opaque copies: the addresses are loop-invariant, and hoisting them out of the
-        // iteration loop (~40 extra live VGPRs) spills
-        uint32_t zb = zb0, cr = cr0;
-        asm volatile("" : "+v"(zb), "+v"(cr));
-        if (hasn) {
-            uint32_t u = wd << (32 - rd);
-            const uint32_t idxo = wd >> 24;
-            const T mA = nA, mB = nB;
-            T min1 = FT<T>::inf(), min2 = FT<T>::inf();
-            uint32_t idx = 0, negs = 0;
-            bool par = false;
-            auto edge = [&](uint32_t q0, T av, T rold) {
-                par ^= av < T(0);
-                const T q = av - rold;
-                const T aq = fabs(q);
-                idx = aq < min1 ? q0 : idx;
-                asm volatile("" : "+v"(idx));
-                negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
-                two_min(min1, min2, aq);
-            };
-            // the row's LQ reads CH at a time, a chunk's all in flight before the first is used
-            sfor<0, (DMAX + CH - 1) / CH>([&](auto cc) {
-                constexpr int c0 = decltype(cc)::value * CH, c1 = c0 + CH < DMAX ? c0 + CH : DMAX;
-                if (c0 < dc) {
-                    T a[CH];
-                    sfor<c0, c1>([&](auto xc) {
-                        constexpr int x = decltype(xc)::value;
-                        if (x < dc) {
-                            const uint32_t Wx = rws[re0 + x];
-                            const uint32_t zz = zb + (Wx >> 17);
-                            a[x - c0] = ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT));
-                        }
-                    });
-                    sfor<c0, c1>([&](auto xc) {
-                        constexpr int x = decltype(xc)::value;
-                        if (x < dc) {
-                            const T rold = xsign_v(idxo == (uint32_t)x ? mB : mA, u, mv);
-                            asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1
-                            edge((uint32_t)x, a[x - c0], rold);
-                        }
-                    });
+        sfor<0, R>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            // per-iteration opaque copy: the addresses are loop-invariant, and hoisting them out of
+            // the iteration loop (~40 extra live VGPRs) spills
+            uint32_t zb = zb0[k];
+            asm volatile("" : "+v"(zb));
+            if (hasn[k]) {
+                const int d = rd[k], dck = dc[k];
+                const uint32_t rb = re0[k];
+                uint32_t u = wd[k] << (32 - d);
+                const uint32_t idxo = wd[k] >> 24;
+                const T mA = nA[k], mB = nB[k];
+                T min1 = FT<T>::inf(), min2 = FT<T>::inf();
+                uint32_t idx = 0, negs = 0;
+                bool par = false;
+                auto edge = [&](uint32_t q0, T av, T rold) {
+                    par ^= av < T(0);
+                    const T q = av - rold;
+                    const T aq = fabs(q);
+                    idx = aq < min1 ? q0 : idx;
+                    asm volatile("" : "+v"(idx));
+                    negs = __builtin_amdgcn_alignbit(negs, FT<T>::sbits(q), 31);
+                    two_min(min1, min2, aq);
+                };
+                // the row's LQ reads CH at a time, a chunk's all in flight before the first is used
+                sfor<0, (DMAX + CH - 1) / CH>([&](auto cc) {
+                    constexpr int c0 = decltype(cc)::value * CH, c1 = c0 + CH < DMAX ? c0 + CH : DMAX;
+                    if (c0 < dck) {
+                        T a[CH];
+                        sfor<c0, c1>([&](auto xc) {
+                            constexpr int x = decltype(xc)::value;
+                            if (x < dck) {
+                                const uint32_t Wx = rws[rb + x];
+                                const uint32_t zz = zb + (Wx >> 17);
+                                a[x - c0] = ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT));
+                            }
+                        });
+                        sfor<c0, c1>([&](auto xc) {
+                            constexpr int x = decltype(xc)::value;
+                            if (x < dck) {
+                                const T rold = xsign_v(idxo == (uint32_t)x ? mB : mA, u, mv);
+                                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1
+                                edge((uint32_t)x, a[x - c0], rold);
+                            }
+                        });
+                    }
+                });
+                if (xe[k]) {   // the extension edge (the row's last): LQ of the degree-1 column = LLR + its r
+                    const T rold = xsign_v(idxo == (uint32_t)dck ? mB : mA, wd[k] << 31, mv);
+                    const T av = xl[k] + rold;
+                    hdx[k] = av < T(0);
+                    edge((uint32_t)dck, av, rold);
                 }
-            });
-            if (xe) {   // the extension edge (the row's last): LQ of the degree-1 column = LLR + its r
-                const T rold = xsign_v(idxo == (uint32_t)dc ? mB : mA, wd << 31, mv);
-                const T av = xl + rold;
-                hdx = av < T(0);
-                edge((uint32_t)dc, av, rold);
-            }
-            fail = par;
-            T x1 = min1, x2 = min2;
-            if constexpr (OFS) {
-                x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
-                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
-            }
-            const uint32_t sgn = 0u - (__builtin_popcount(negs) & 1u);   // row sign product
-            const uint32_t flip = sgn & ((1u << rd) - 1u);
-            nA = alpha * x1, nB = alpha * x2;
-            wd = (negs ^ flip) | (idx << 24);
-            uint32_t un = wd << (32 - rd);
-            sfor<0, DMAX>([&](auto xc) {
-                constexpr int x = decltype(xc)::value;
-                if (x < dc) {
-                    const uint32_t V = wws[re0 + x];
-                    const T r = xsign_v(idx == (uint32_t)x ? nB : nA, un, mv);
-                    asm("v_add_u32 %0, %1, %1" : "=v"(un) : "v"(un));
-                    const uint32_t zz = zb + (V >> 20);
-                    st_sc1(msg, (V & 0xfffffu) + min(zz, zz - ZT), r);
+                fail |= par;
+                T x1 = min1, x2 = min2;
+                if constexpr (OFS) {
+                    x1 = min1 - beta, x2 = min2 - beta;   // max(minv - beta, 0) (:201)
+                    x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
                 }
-            });
-        }
+                const uint32_t sgn = 0u - (__builtin_popcount(negs) & 1u);   // row sign product
+                const uint32_t flip = sgn & ((1u << d) - 1u);
+                const T nAk = alpha * x1, nBk = alpha * x2;
+                nA[k] = nAk, nB[k] = nBk;
+                wd[k] = (negs ^ flip) | (idx << 24);
+                uint32_t un = wd[k] << (32 - d);
+                sfor<0, DMAX>([&](auto xc) {
+                    constexpr int x = decltype(xc)::value;
+                    if (x < dck) {
+                        const uint32_t V = wws[rb + x];
+                        const T r = xsign_v(idx == (uint32_t)x ? nBk : nAk, un, mv);
+                        asm("v_add_u32 %0, %1, %1" : "=v"(un) : "v"(un));
+                        const uint32_t zz = zb + (V >> 20);
+                        st_sc1(msg, (V & 0xfffffu) + min(zz, zz - ZT), r);
+                    }
+                });
+            }
+        });
         if (fail) lfail = (uint32_t)(it + 1);
         if (it < 2) SPLIT_TS(2 + 4 * it);
         grid_sync(1, (uint32_t)(it + 1));
         if (it < 2) SPLIT_TS(3 + 4 * it);
         if (lflag != (uint32_t)(it + 1)) {
             // ---- the syndrome of LQ_old holds (:112-114): its hard decisions are the output
-            if (hasc) crow[cj * Zc + cz] = (int8_t)(lqv < T(0));
-            if (hasn && xe) crow[(KB + ri) * Zc + rz] = (int8_t)hdx;
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                if (hasc[k]) crow[cj[k] * Zc + cz[k]] = (int8_t)(lqv[k] < T(0));
+                if (hasn[k] && xe[k]) crow[(KB + ri[k]) * Zc + rz[k]] = (int8_t)hdx[k];
+            }
             if (w == 0 && t == 0) status[cb] = 1, iters[cb] = it;
             return;
         }
-        // ---- phase B: LQ = LLRin + Lr.sum(axis=0) (:126), rows ascending: the wave's column
-        if (hasc) {
-            T acc = T(0);
-            sfor<0, (CMAX + CCH - 1) / CCH>([&](auto cc) {
-                constexpr int p0 = decltype(cc)::value * CCH, p1 = p0 + CCH < CMAX ? p0 + CCH : CMAX;
-                if (p0 < cn) {
-                    T m[CCH];
-                    sfor<p0, p1>([&](auto pc_) {
-                        constexpr int p = decltype(pc_)::value;
-                        if (p < cn) m[p - p0] = ld_sc1(msg, cr + (uint32_t)p * ZT);
-                    });
-                    sfor<p0, p1>([&](auto pc_) {
-                        constexpr int p = decltype(pc_)::value;
-                        if (p < cn) acc = acc + m[p - p0];
-                    });
-                }
-            });
-            lqv = (cpun ? T(0) : lf) + acc;   // punctured columns: LLR 0 (:43)
-            st_sc1(lq, cq, lqv);
-        }
+        // ---- phase B: LQ = LLRin + Lr.sum(axis=0) (:126), rows ascending: each chunk's column
+        sfor<0, R>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            uint32_t cr = cr0[k];
+            asm volatile("" : "+v"(cr));
+            if (hasc[k]) {
+                const int n = cn[k];
+                T acc = T(0);
+                sfor<0, (CMAX + CCH - 1) / CCH>([&](auto cc) {
+                    constexpr int p0 = decltype(cc)::value * CCH, p1 = p0 + CCH < CMAX ? p0 + CCH : CMAX;
+                    if (p0 < n) {
+                        T m[CCH];
+                        sfor<p0, p1>([&](auto pc_) {
+                            constexpr int p = decltype(pc_)::value;
+                            if (p < n) m[p - p0] = ld_sc1(msg, cr + (uint32_t)p * ZT);
+                        });
+                        sfor<p0, p1>([&](auto pc_) {
+                            constexpr int p = decltype(pc_)::value;
+                            if (p < n) acc = acc + m[p - p0];
+                        });
+                    }
+                });
+                lqv[k] = (cpun[k] ? T(0) : lf[k]) + acc;   // punctured columns: LLR 0 (:43)
+                st_sc1(lq, cq[k], lqv[k]);
+            }
+        });
         if (it < 2) SPLIT_TS(4 + 4 * it);
         grid_sync(1, 0u);
         if (it < 2) SPLIT_TS(5 + 4 * it);
@@ -307,30 +332,38 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
 
     // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
     SPLIT_TS(10);
-    bool ox = false;
-    if (hasn) {
-        bool par = false;
-        if (xe) {
-            const T rx = xsign_v((wd >> 24) == (uint32_t)dc ? nB : nA, wd << 31, mv);
-            ox = xl + rx <= T(0);
-            par = ox;
-        }
-        sfor<0, DMAX>([&](auto xc) {
-            constexpr int x = decltype(xc)::value;
-            if (x < dc) {
-                const uint32_t Wx = rws[re0 + x];
-                const uint32_t zz = zb0 + (Wx >> 17);
-                par ^= ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT)) <= T(0);
+    bool ox[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        ox[k] = false;
+        if (hasn[k]) {
+            bool par = false;
+            const int dck = dc[k];
+            if (xe[k]) {
+                const T rx = xsign_v((wd[k] >> 24) == (uint32_t)dck ? nB[k] : nA[k], wd[k] << 31, mv);
+                ox[k] = xl[k] + rx <= T(0);
+                par = ox[k];
             }
-        });
-        if (par) lfail = (uint32_t)(L + 1);
+            sfor<0, DMAX>([&](auto xc) {
+                constexpr int x = decltype(xc)::value;
+                if (x < dck) {
+                    const uint32_t Wx = rws[re0[k] + x];
+                    const uint32_t zz = zb0[k] + (Wx >> 17);
+                    par ^= ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT)) <= T(0);
+                }
+            });
+            if (par) lfail = (uint32_t)(L + 1);
+        }
     }
     SPLIT_TS(11);
     // ---- the decisions need no barrier; the status does: every workgroup raises its fail flag and
     //      then adds to the counter, and the workgroup whose add comes last (told by the value the
     //      add returns) reads the flag and writes the status — nobody waits
-    if (hasc) crow[cj * Zc + cz] = (int8_t)(lqv <= T(0));
-    if (hasn && xe) crow[(KB + ri) * Zc + rz] = (int8_t)ox;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        if (hasc[k]) crow[cj[k] * Zc + cz[k]] = (int8_t)(lqv[k] <= T(0));
+        if (hasn[k] && xe[k]) crow[(KB + ri[k]) * Zc + rz[k]] = (int8_t)ox[k];
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -353,8 +386,9 @@ template <int BG>
 int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
                    int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
                    hipStream_t st) {
-    const int W = split_parts(BG, Zc);
-    if (B * W > kSplitMaxWG) return fail(LDPC5G_ESIZE, "split decoder: %d x %d workgroups", B, W);
+    const int R = split_wanted(BG, B, Zc);
+    if (R == 0) return fail(LDPC5G_ESIZE, "split decoder: %d codeblocks of Zc=%d do not fit", B, Zc);
+    const int W = split_parts(BG, Zc, R);
     static std::atomic<uint64_t> pool_set{0};   // keep freed pool memory mapped (per device)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -384,7 +418,8 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
         if (!ev) rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate (split chain)");
         else rc = check_hip(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent (split chain)");
         if (!rc) {
-            auto kern = beta != 0.0 ? ldpc_split_kernel<BG, true> : ldpc_split_kernel<BG, false>;
+            auto kern = R == 1 ? (beta != 0.0 ? ldpc_split_kernel<BG, true, 1> : ldpc_split_kernel<BG, false, 1>)
+                               : (beta != 0.0 ? ldpc_split_kernel<BG, true, 2> : ldpc_split_kernel<BG, false, 2>);
             hipLaunchKernelGGL(kern, dim3(B * W), dim3(kSplitThreads), 0, st, llr, ck, status, iters, Zc, zi, W,
                                ldl, ldc, L, alpha, beta, pc, (double*)p, sync);
             rc = check_hip(hipGetLastError(), "ldpc_split_kernel launch");
@@ -397,17 +432,20 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
 
 }  // namespace
 
-int split_parts(int bgn, int Zc) {   // 64-slot row chunks over 16-wave workgroups
+int split_parts(int bgn, int Zc, int R) {   // 64-slot row chunks, R per wave, 16-wave workgroups
     const int mb = bgn == 1 ? BGT<1>::MB : BGT<2>::MB;
-    return (mb * ((Zc + 63) / 64) + kSplitThreads / 64 - 1) / (kSplitThreads / 64);
+    const int per = R * (kSplitThreads / 64);
+    return (mb * ((Zc + 63) / 64) + per - 1) / per;
 }
 
-bool split_wanted(int bgn, int B, int Zc) {
+int split_wanted(int bgn, int B, int Zc) {
     // LDPC5G_NO_SPLIT=1: the one-workgroup-per-codeblock kernels instead (A/B measurements)
     static const bool off = [] { const char* e = getenv("LDPC5G_NO_SPLIT"); return e && *e && *e != '0'; }();
     // BG2 Zc <= 64 keeps the small-codeblock kernel (its LDS image fits one CU)
-    if (off || Zc < 64 || (bgn == 2 && Zc <= 64)) return false;
-    return B * split_parts(bgn, Zc) <= kSplitMaxWG;
+    if (off || B < 1 || Zc < 64 || (bgn == 2 && Zc <= 64)) return 0;
+    if (B * split_parts(bgn, Zc, 1) <= kSplitMaxWG) return 1;
+    if (B * split_parts(bgn, Zc, 2) <= kSplitMaxWG) return 2;
+    return 0;
 }
 
 int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,

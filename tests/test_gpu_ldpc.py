@@ -226,7 +226,8 @@ def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
     mixed SNRs, and rate-matched rows (untransmitted extension columns +0.0: the dead-row
     variants), bit-exact with the oracle."""
     rng = np.random.default_rng(7 + rm + 10 * bg)
-    Zc, B = 384, 9   # float64: 9 codeblocks run the batch kernels (7 would take the split kernel)
+    # float64: 30 codeblocks run the batch kernels (up to 24 BG1 / 28 BG2 take the split kernel)
+    Zc, B = 384, (30 if dtype == np.float64 else 9)
     ck = rng.integers(0, 2, (B, (22 if bg == 1 else 10) * Zc)).astype(np.int8)
     dn = O.encode(ck, bg)
     snr = rng.choice([-1.0, 1.0, 3.0], size=B)[:, None]
@@ -242,11 +243,14 @@ def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
 
 
 @pytest.mark.parametrize("bg,Zc,B", [(1, 384, 1), (2, 384, 1), (1, 384, 7), (1, 64, 1), (1, 96, 2),
-                                     (2, 72, 1), (2, 176, 3), (1, 208, 1), (2, 384, 8)])
+                                     (2, 72, 1), (2, 176, 3), (1, 208, 1), (2, 384, 8),
+                                     # two chunks per wave (R = 2): more codeblocks than R = 1 fits
+                                     (1, 384, 23), (2, 384, 15), (1, 208, 30), (1, 120, 40)])
 def test_decode_split_kernel_vs_oracle(torch, dec, bg, Zc, B):
     """The multi-workgroup float64 flooding kernel (ldpc5g_dec_split.hip: each codeblock over
     ceil(MB*Zc/1024) CUs, barriers over a codeblock's workgroups) that serves launches of a few
-    large codeblocks (the per-codeblock drop-ins), bit-exact with the oracle: NMS and OMS,
+    large codeblocks (the per-codeblock drop-ins and whole transport blocks of up to 24 BG1 Zc=384
+    codeblocks: one or two 64-slot chunks per wave), bit-exact with the oracle: NMS and OMS,
     L = 0 / 1 / 8, integer LLRs (|q| ties), an all-zero codeblock, a noiseless one, mixed SNRs
     (codeblocks of one launch exiting at different iterations) and rate-matched rows."""
     rng = np.random.default_rng(Zc * 3 + B + 100 * bg)
