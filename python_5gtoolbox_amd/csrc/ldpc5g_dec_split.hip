@@ -101,6 +101,13 @@ struct SplitPlan {
 template <int BG>
 __device__ constexpr SplitPlan<BG> kSplitPlanD{};
 
+// a codeblock's sync words back to zero (sc1 vector stores; the next split launch of the device
+// starts after this kernel ends — the launcher's chain)
+__device__ inline void sync_clear(uint32_t* sy) {
+    for (int k = 0; k < 4; ++k)
+        __hip_atomic_store((g_u32*)(uintptr_t)(sy + k), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // R chunks per wave (R = 2 halves the workgroups per codeblock, so twice as many codeblocks fit
 // one launch): wave v of workgroup w owns chunks of rounds v*R .. v*R + R-1, each round dealt
 // snake-wise as above; the chunks of a wave are walked one after the other in each phase.
@@ -131,7 +138,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     const uint32_t ZT = (uint32_t)(Zc * TS);
     double* lq = scratch + (size_t)cb * split_rows<BG>() * Zc;   // [KC][Zc] LQ of the core columns
     double* msg = lq + (size_t)KC * Zc;                            // [NCE][Zc] messages, CSC slots
-    uint32_t* sy = sync + cb * kSplitSync;   // [0] barrier counter, [1] fail tag, [2] final fail
+    uint32_t* sy = sync + cb * kSplitSync;   // [0] barrier counter, [1] fail tag, [2] final fail, [3] exits
 
     // barrier over the codeblock's W workgroups.  sig: this workgroup's fail tag (LDS lfail) is
     // raised into sy[fi] first; afterwards lflag = sy[fi] for every thread of the workgroup.
@@ -297,6 +304,11 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
                 if (hasn[k] && xe[k]) crow[(KB + ri[k]) * Zc + rz[k]] = (int8_t)hdx[k];
             }
             if (w == 0 && t == 0) status[cb] = 1, iters[cb] = it;
+            // the sync words go back to zero for the next launch: the last workgroup to leave (every
+            // one has read sy[1] by now) clears them
+            if (t == 0 && __hip_atomic_fetch_add((g_u32*)(uintptr_t)(sy + 3), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(W - 1))
+                sync_clear(sy);
             return;
         }
         // ---- phase B: LQ = LLRin + Lr.sum(axis=0) (:126), rows ascending: each chunk's column
@@ -372,7 +384,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         const uint32_t old = __hip_atomic_fetch_add((g_u32*)(uintptr_t)sy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == nbar + (uint32_t)W) status[cb] = ld_sc1(sy + 2) == 0u, iters[cb] = L;
+        if (old + 1u == nbar + (uint32_t)W) status[cb] = ld_sc1(sy + 2) == 0u, iters[cb] = L, sync_clear(sy);
     }
     SPLIT_TS(12);
 #ifdef LDPC5G_SPLIT_TS
@@ -400,23 +412,36 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
         }
         pool_set.fetch_or(1ull << (dev & 63), std::memory_order_release);
     }
-    const size_t data = (size_t)B * split_rows<BG>() * Zc * sizeof(double);
-    const size_t bytes = data + (size_t)B * kSplitSync * 4;
+    const size_t bytes = (size_t)B * split_rows<BG>() * Zc * sizeof(double);
     void* p = nullptr;
     if (int rc = check_hip(hipMallocAsync(&p, bytes, st), "hipMallocAsync (split decoder scratch)")) return rc;
-    uint32_t* sync = (uint32_t*)((char*)p + data);
-    int rc = check_hip(hipMemsetAsync(sync, 0, (size_t)B * kSplitSync * 4, st), "hipMemsetAsync");
-    if (!rc) {
+    int rc = 0;
+    {
         // split launches of one device run one after another, whatever their streams: each needs
         // all of its <= kSplitMaxWG workgroups resident together, and two or more launches sharing
         // the CUs could each hold part of the chip while waiting for the rest (their barriers would
         // never complete).  A per-device event chain orders them; on one stream it costs nothing.
+        // The chain also lets them share one sync area per device, zeroed once: every launch leaves
+        // its words zero again (sync_clear), so no memset sits before the kernel.
         static std::mutex mu;
         static hipEvent_t last[64] = {};
+        static uint32_t* sync_area[64] = {};
         std::lock_guard<std::mutex> lk(mu);
         hipEvent_t& ev = last[dev & 63];
-        if (!ev) rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate (split chain)");
-        else rc = check_hip(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent (split chain)");
+        uint32_t*& sync = sync_area[dev & 63];
+        if (!sync) {
+            const size_t sb = (size_t)kSplitMaxWG * kSplitSync * 4;
+            void* q = nullptr;
+            rc = check_hip(hipMalloc(&q, sb), "hipMalloc (split sync area)");
+            if (!rc) rc = check_hip(hipMemset(q, 0, sb), "hipMemset (split sync area)");
+            if (!rc) sync = (uint32_t*)q;
+        }
+        if (rc) {
+        } else if (!ev) {
+            rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate (split chain)");
+        } else {
+            rc = check_hip(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent (split chain)");
+        }
         if (!rc) {
             auto kern = R == 1 ? (beta != 0.0 ? ldpc_split_kernel<BG, true, 1> : ldpc_split_kernel<BG, false, 1>)
                                : (beta != 0.0 ? ldpc_split_kernel<BG, true, 2> : ldpc_split_kernel<BG, false, 2>);
