@@ -18,10 +18,12 @@
 // `sc1` (write-through) store, every storing wave drains (vmcnt(0)) before the workgroup barrier
 // behind which one lane adds to the counter, the counter is polled with an `sc1` load and every load
 // of hand-off data is an `sc1` global load (MI355X_MICROARCH.md, hand-off table first row): no L2
-// write-back or L1 invalidate fence on the critical path.  All W*B workgroups must be resident
-// together: the launcher keeps B*W <= kSplitMaxWG (224 of the 256 CUs), one workgroup per CU, and
-// chains the split launches of a device one after another across streams (an event per device).
-// Launches of more codeblocks take R = 2 chunks per wave (half the workgroups per codeblock).
+// write-back or L1 invalidate fence on the critical path.  A codeblock's W workgroups must be
+// resident together: workgroups take their (codeblock, part) by an arrival ticket, so parts go to
+// resident workgroups in order and at most one codeblock per launch waits for CUs; the launcher keeps
+// B*W <= kSplitMaxWG (224 of the 256 CUs), one workgroup per CU, and chains the split launches of a
+// device (in one process) one after another across streams (an event per device).  Launches of
+// more codeblocks take R = 2 chunks per wave (half the workgroups per codeblock).
 #include <stdlib.h>
 
 #include <mutex>
@@ -43,7 +45,8 @@ constexpr int kSplitMaxWG = 224;   // of the 256 CUs, one workgroup each
 #define LDPC5G_SPLIT_CCH 32
 #endif
 // development instrumentation (tools/split_probe.py): workgroup 0 thread 0's real-time clock
-// (100 MHz) at phase boundaries, dumped over codeblock 0's decisions
+// (100 MHz) at phase boundaries, dumped over its codeblock's decisions (codeblock 0 when workgroup 0
+// takes the first ticket, as it does when dispatched first)
 #ifdef LDPC5G_SPLIT_TS
 #define SPLIT_TS(n) \
     if (g == 0 && (n) < 16) tsv[(n)] = __builtin_amdgcn_s_memrealtime()
@@ -115,7 +118,8 @@ template <int BG, bool OFS, int R>
 __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int Zc, int zi, int W, int64_t ldl, int64_t ldc, int L, double alpha,
-    double beta, int pc, double* __restrict__ scratch, uint32_t* __restrict__ sync) {
+    double beta, int pc, double* __restrict__ scratch, uint32_t* __restrict__ sync,
+    uint32_t* __restrict__ ticket) {
     using P = BGT<BG>;
     using T = double;
     constexpr int MB = P::MB, KB = P::KB, KC = P::KC, TS = 8;
@@ -123,19 +127,49 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     // loads in flight per chunk (phase A, B); R = 2 keeps twice the chunk state, so fewer
     constexpr int CH = R == 1 ? LDPC5G_SPLIT_CH : 16, CCH = R == 1 ? LDPC5G_SPLIT_CCH : 16;
     __shared__ uint32_t rws[MB * DMAX], wws[MB * DMAX];   // edge words per (row, edge < DMAX)
-    __shared__ uint32_t lfail, lflag;
+    __shared__ uint32_t lfail, lflag, lticket;
 
-    const int cb = blockIdx.x / W, w = blockIdx.x - cb * W;
     const int t = threadIdx.x, lane = t & 63;
     const int v = __builtin_amdgcn_readfirstlane(t >> 6);
 #ifdef LDPC5G_SPLIT_TS
     uint64_t tsv[16] = {};
 #endif
-    const int g = w * kSplitThreads + t;   // (instrumentation: workgroup 0, thread 0)
+    const int g = blockIdx.x * kSplitThreads + t;   // (instrumentation: workgroup 0, thread 0)
     SPLIT_TS(0);
+    // (codeblock, part) by arrival ticket, not by blockIdx: the parts of a codeblock go to
+    // workgroups that are resident, so at most one codeblock of the launch has some of its parts
+    // waiting for CUs while the others run to completion and free theirs — two processes sharing
+    // the GPU cannot each hold part of the chip waiting for the rest.  The ticket is taken here and
+    // read after the edge-word fill (its round trip overlaps it).
+    uint32_t tk = 0u;
+    if (t == 0) tk = __hip_atomic_fetch_add((g_u32*)(uintptr_t)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ZT = (uint32_t)(Zc * TS);
+
+    // ---- edge words: read word = column byte offset | (V mod Zc)*8 << 17; write word = CSC slot
+    //      byte offset | (V mod Zc)*8 << 20
+    for (int q = t; q < MB * DMAX; q += kSplitThreads) {
+        const int i = q / DMAX, x = q - i * DMAX;
+        const int e0 = row_start_d<BG>(i), dc = row_start_d<BG>(i + 1) - e0 - (i >= 4 ? 1 : 0);
+        uint32_t rw = 0u, ww = 0u;
+        if (x < dc) {
+            const uint32_t w0 = kSmallPlanD<BG>.ew[e0 + x];
+            const uint32_t sb = (uint32_t)shift_of<BG>(zi, e0 + x) * TS;
+            rw = (w0 & 0xffu) * ZT | (sb << 17);
+            ww = (w0 >> 8) * ZT | (sb << 20);
+        }
+        rws[q] = rw, wws[q] = ww;
+    }
+    if (t == 0) {
+        // the last ticket of the launch: every workgroup holds its own, the counter goes back to 0
+        if (tk == gridDim.x - 1u)
+            __hip_atomic_store((g_u32*)(uintptr_t)ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lticket = tk, lfail = 0u;
+    }
+    __syncthreads();
+    const int tkt = __builtin_amdgcn_readfirstlane((int)lticket);
+    const int cb = tkt / W, w = tkt - cb * W;
     const T* lrow = llr + (int64_t)cb * ldl;
     int8_t* crow = ck + (int64_t)cb * ldc;
-    const uint32_t ZT = (uint32_t)(Zc * TS);
     double* lq = scratch + (size_t)cb * split_rows<BG>() * Zc;   // [KC][Zc] LQ of the core columns
     double* msg = lq + (size_t)KC * Zc;                            // [NCE][Zc] messages, CSC slots
     uint32_t* sy = sync + cb * kSplitSync;   // [0] barrier counter, [1] fail tag, [2] final fail, [3] exits
@@ -159,21 +193,6 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
         __syncthreads();
     };
 
-    // ---- edge words: read word = column byte offset | (V mod Zc)*8 << 17; write word = CSC slot
-    //      byte offset | (V mod Zc)*8 << 20
-    for (int q = t; q < MB * DMAX; q += kSplitThreads) {
-        const int i = q / DMAX, x = q - i * DMAX;
-        const int e0 = row_start_d<BG>(i), dc = row_start_d<BG>(i + 1) - e0 - (i >= 4 ? 1 : 0);
-        uint32_t rw = 0u, ww = 0u;
-        if (x < dc) {
-            const uint32_t w0 = kSmallPlanD<BG>.ew[e0 + x];
-            const uint32_t sb = (uint32_t)shift_of<BG>(zi, e0 + x) * TS;
-            rw = (w0 & 0xffu) * ZT | (sb << 17);
-            ww = (w0 >> 8) * ZT | (sb << 20);
-        }
-        rws[q] = rw, wws[q] = ww;
-    }
-    if (t == 0) lfail = 0u;
     const int nch = (Zc + 63) >> 6;   // chunks per row / column
     // per chunk slot k < R: own core column entry (cj, cz) and own check node (ri, rz)
     int cj[R], cn[R], ri[R], rd[R], dc[R], cz[R], rz[R];
@@ -430,7 +449,7 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
         hipEvent_t& ev = last[dev & 63];
         uint32_t*& sync = sync_area[dev & 63];
         if (!sync) {
-            const size_t sb = (size_t)kSplitMaxWG * kSplitSync * 4;
+            const size_t sb = ((size_t)kSplitMaxWG + 1) * kSplitSync * 4;   // + the ticket line
             void* q = nullptr;
             rc = check_hip(hipMalloc(&q, sb), "hipMalloc (split sync area)");
             if (!rc) rc = check_hip(hipMemset(q, 0, sb), "hipMemset (split sync area)");
@@ -446,7 +465,7 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
             auto kern = R == 1 ? (beta != 0.0 ? ldpc_split_kernel<BG, true, 1> : ldpc_split_kernel<BG, false, 1>)
                                : (beta != 0.0 ? ldpc_split_kernel<BG, true, 2> : ldpc_split_kernel<BG, false, 2>);
             hipLaunchKernelGGL(kern, dim3(B * W), dim3(kSplitThreads), 0, st, llr, ck, status, iters, Zc, zi, W,
-                               ldl, ldc, L, alpha, beta, pc, (double*)p, sync);
+                               ldl, ldc, L, alpha, beta, pc, (double*)p, sync, sync + kSplitMaxWG * kSplitSync);
             rc = check_hip(hipGetLastError(), "ldpc_split_kernel launch");
             if (!rc) rc = check_hip(hipEventRecord(ev, st), "hipEventRecord (split chain)");
         }

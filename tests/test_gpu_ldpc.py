@@ -9,6 +9,7 @@ Bars:
   full-size (4096 x BG1 Zc=384): codeword syndrome == 0, encode->BPSK->decode round trip
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -299,6 +300,20 @@ def test_decode_split_kernel_concurrent_streams(torch, dec):
     for o, r in zip(outs, ref):
         for a, b in zip(o, r):
             assert torch.equal(a.cpu(), b)
+
+
+def test_decode_split_kernel_two_processes(torch):
+    """Two processes on the GPU launching the multi-workgroup kernel at once, 12 BG1 Zc=384
+    codeblocks = 216 workgroups per launch (two launches cannot be resident together): parts are
+    taken by arrival ticket, so both finish, every repetition equal to the first
+    (tools/split_mp_probe.py; the children are new interpreters, started under a time limit)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "split_mp_probe.py"), "2", "300"],
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.stdout.count("mismatches 0") == 2, r.stdout
 
 
 def test_decode_ldpc_full_length(torch, dec):
