@@ -26,6 +26,7 @@
 // more codeblocks take R = 2 chunks per wave (half the workgroups per codeblock).
 #include <stdlib.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "ldpc5g_dec_small.h"
@@ -420,40 +421,43 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
     const int R = split_wanted(BG, B, Zc);
     if (R == 0) return fail(LDPC5G_ESIZE, "split decoder: %d codeblocks of Zc=%d do not fit", B, Zc);
     const int W = split_parts(BG, Zc, R);
-    static std::atomic<uint64_t> pool_set{0};   // keep freed pool memory mapped (per device)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (!(pool_set.load(std::memory_order_acquire) & (1ull << (dev & 63)))) {
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-            uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
-        pool_set.fetch_or(1ull << (dev & 63), std::memory_order_release);
-    }
     const size_t bytes = (size_t)B * split_rows<BG>() * Zc * sizeof(double);
-    void* p = nullptr;
-    if (int rc = check_hip(hipMallocAsync(&p, bytes, st), "hipMallocAsync (split decoder scratch)")) return rc;
     int rc = 0;
     {
-        // split launches of one device run one after another, whatever their streams: each needs
-        // all of its <= kSplitMaxWG workgroups resident together, and two or more launches sharing
-        // the CUs could each hold part of the chip while waiting for the rest (their barriers would
-        // never complete).  A per-device event chain orders them; on one stream it costs nothing.
-        // The chain also lets them share one sync area per device, zeroed once: every launch leaves
-        // its words zero again (sync_clear), so no memset sits before the kernel.
+        // split launches of one device run one after another, whatever their streams (a per-device
+        // event chain; on one stream it costs nothing), so they share one scratch and one sync area
+        // per device, plain hipMalloc memory (the hand-off table's row): the scratch grows on
+        // demand (after the previous launch has ended), the sync area is zeroed once and every
+        // launch leaves its words zero again (sync_clear), so no allocation or memset runs per call
         static std::mutex mu;
         static hipEvent_t last[64] = {};
         static uint32_t* sync_area[64] = {};
+        static void* scratch_area[64] = {};
+        static size_t scratch_cap[64] = {};
         std::lock_guard<std::mutex> lk(mu);
         hipEvent_t& ev = last[dev & 63];
         uint32_t*& sync = sync_area[dev & 63];
+        void*& p = scratch_area[dev & 63];
         if (!sync) {
             const size_t sb = ((size_t)kSplitMaxWG + 1) * kSplitSync * 4;   // + the ticket line
             void* q = nullptr;
             rc = check_hip(hipMalloc(&q, sb), "hipMalloc (split sync area)");
             if (!rc) rc = check_hip(hipMemset(q, 0, sb), "hipMemset (split sync area)");
+            if (!rc) rc = check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (split sync area)");
             if (!rc) sync = (uint32_t*)q;
+        }
+        if (!rc && scratch_cap[dev & 63] < bytes) {
+            if (p) {
+                if (ev) rc = check_hip(hipEventSynchronize(ev), "hipEventSynchronize (split scratch)");
+                if (!rc) rc = check_hip(hipFree(p), "hipFree (split scratch)");
+                p = nullptr, scratch_cap[dev & 63] = 0;
+            }
+            // at least 24 BG1 Zc = 384 codeblocks' worth (20 MB), so most devices allocate once
+            const size_t want = std::max(bytes, (size_t)24 * split_rows<1>() * 384 * sizeof(double));
+            if (!rc) rc = check_hip(hipMalloc(&p, want), "hipMalloc (split scratch)");
+            if (!rc) scratch_cap[dev & 63] = want;
         }
         if (rc) {
         } else if (!ev) {
@@ -470,8 +474,7 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
             if (!rc) rc = check_hip(hipEventRecord(ev, st), "hipEventRecord (split chain)");
         }
     }
-    const int rf = check_hip(hipFreeAsync(p, st), "hipFreeAsync");
-    return rc ? rc : rf;
+    return rc;
 }
 
 }  // namespace
