@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "ldpc5g_dec_small.h"
@@ -36,7 +37,7 @@ namespace {
 
 constexpr int kSplitThreads = 1024;
 constexpr int kSplitSync = 64;   // sync words per codeblock (a 256-B line): barrier counter, flags
-constexpr int kSplitMaxWG = 224;   // of the 256 CUs, one workgroup each
+constexpr int kSplitMaxWG = 224;   // of the 256 CUs, one workgroup each (7/8 of a device's CUs)
 // loads in flight per chunk (phase A LQ reads, phase B message reads); 32: a row's / column's all
 // at once (r05, one BG1 Zc=384 codeblock: 10 / 10 100 us per call, all 87 us)
 #ifndef LDPC5G_SPLIT_CH
@@ -490,8 +491,20 @@ int split_wanted(int bgn, int B, int Zc) {
     static const bool off = [] { const char* e = getenv("LDPC5G_NO_SPLIT"); return e && *e && *e != '0'; }();
     // BG2 Zc <= 64 keeps the small-codeblock kernel (its LDS image fits one CU)
     if (off || B < 1 || Zc < 64 || (bgn == 2 && Zc <= 64)) return 0;
-    if (B * split_parts(bgn, Zc, 1) <= kSplitMaxWG) return 1;
-    if (B * split_parts(bgn, Zc, 2) <= kSplitMaxWG) return 2;
+    // the launch fills at most 7/8 of the device's CUs (224 of 256; a partitioned device has fewer),
+    // and a codeblock's W workgroups must fit the device at once
+    static std::atomic<int> cus_of[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    int cus = cus_of[dev & 63].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
+        cus_of[dev & 63].store(cus, std::memory_order_relaxed);
+    }
+    const int maxwg = std::min(kSplitMaxWG, cus * 7 / 8);
+    const int w1 = split_parts(bgn, Zc, 1), w2 = split_parts(bgn, Zc, 2);
+    if (w1 <= cus && B * w1 <= maxwg) return 1;
+    if (w2 <= cus && B * w2 <= maxwg) return 2;
     return 0;
 }
 
