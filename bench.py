@@ -352,6 +352,24 @@ def bench_single_cb(torch, rank):
         host_us = (time.perf_counter() - t0) / 50 * 1e6
         res[f"bg{bg}"] = {"device_us_per_call": round(us, 1), "dropin_host_us_per_call": round(host_us, 1),
                           "iterations": int(out[2].item())}
+    # a whole BG1 transport block of 23 Zc=384 codeblocks in one call (DLSCHDecode swapped whole, or
+    # sch_decode_batch): the multi-workgroup kernel with two chunks per wave, 207 workgroups; beside
+    # it the one-workgroup-per-codeblock batch kernel's time for the same call is ~220 us
+    B, Zc = 23, 384
+    K, N, Nf = code_dims(1, Zc)
+    ck = torch.randint(0, 2, (B, K), dtype=torch.int8, device="cuda", generator=g)
+    dn = E.encode_ldpc_batch(ck, 1)
+    sigma = 10 ** (3 / 20)
+    llr = (2 * ((1 - 2 * dn.double()) + sigma * torch.randn(dn.shape, dtype=torch.float64, device="cuda",
+                                                              generator=g)) / sigma ** 2).contiguous()
+    out = (torch.empty((B, Nf), dtype=torch.int8, device="cuda"), torch.empty((B,), dtype=torch.uint8, device="cuda"),
+           torch.empty((B,), dtype=torch.int32, device="cuda"))
+    fn = lambda: D.nr_decode_ldpc_batch(llr, Zc, 1, 8, "min-sum", 0.75, 0.0, "flooding", out=out)  # noqa: E731
+    for _ in range(10):
+        fn()
+    us = ev_ms(torch, fn, reps=200) * 1e3
+    res["bg1_tb23"] = {"device_us_per_call": round(us, 1), "codeblocks": B,
+                       "max_iterations": int(out[2].max().item())}
     return res
 
 
