@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 
 #include "ldpc5g_dec_small.h"
 
@@ -229,13 +230,19 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     }
     uint32_t mv = 0x80000000u;
     asm volatile("" : "+v"(mv));
-    grid_sync(1, 0u);
+    // iteration 0's phase A reads LQ_0 = the LLRs straight from the input (punctured columns 0), so
+    // no barrier is needed before it; only L = 0 reads the scratch LQ (the final pass) right away
+    if (L == 0) grid_sync(1, 0u);
     SPLIT_TS(1);
+    const uint32_t pcZT = (uint32_t)pc * ZT;
+    const char* lrowb = (const char*)lrow - pcZT;   // byte offset col*ZT + z*8 of LQ_0 (col >= pc)
 
     int it = 0;
     for (; it < L; ++it) {
         // ---- phase A (rows from LQ_old, syndrome of LQ_old): each chunk's row, its dc core edges
         bool fail = false;
+        auto phase_a = [&](auto firstc) {
+        constexpr bool FIRST = decltype(firstc)::value;
         sfor<0, R>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             // per-iteration opaque copy: the addresses are loop-invariant, and hoisting them out of
@@ -270,7 +277,11 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
                             if (x < dck) {
                                 const uint32_t Wx = rws[rb + x];
                                 const uint32_t zz = zb + (Wx >> 17);
-                                a[x - c0] = ld_sc1(lq, (Wx & 0x1ffffu) + min(zz, zz - ZT));
+                                const uint32_t off = (Wx & 0x1ffffu) + min(zz, zz - ZT);
+                                if constexpr (FIRST)
+                                    a[x - c0] = off >= pcZT ? *(const g_f64*)(uintptr_t)(lrowb + off) : T(0);
+                                else
+                                    a[x - c0] = ld_sc1(lq, off);
                             }
                         });
                         sfor<c0, c1>([&](auto xc) {
@@ -313,6 +324,11 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
                 });
             }
         });
+        };
+        if (it == 0)
+            phase_a(std::true_type{});
+        else
+            phase_a(std::false_type{});
         if (fail) lfail = (uint32_t)(it + 1);
         if (it < 2) SPLIT_TS(2 + 4 * it);
         grid_sync(1, (uint32_t)(it + 1));
