@@ -197,12 +197,52 @@ def _cpu_worker(job):
             return done, el
 
 
+def host_info():
+    """The host the CPU baseline runs on: CPU model, physical cores (sockets x cores per socket
+    from /proc/cpuinfo), logical CPUs, and the CPUs this process may run on."""
+    import platform
+    model, phys = platform.processor() or platform.machine(), set()
+    try:
+        pid = core = None
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name":
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    core = v
+                elif not k and pid is not None:
+                    phys.add((pid, core))
+                    pid = core = None
+            if pid is not None:
+                phys.add((pid, core))
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count()
+    return {"model": model, "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": aff}
+
+
+def _host_cpu():
+    h = host_info()
+    return (f"host {h['model']}, {h['physical_cores']} physical cores / {h['logical_cpus']} logical "
+            f"CPUs ({h['affinity_cpus']} in this process's affinity)")
+
+
 def cpu_baseline(seconds, schedule, alpha, L, procs):
     """Oracle (numpy restatement, kind "port") on a bounded sample of the same workload, one
     process per host core up to `procs`.  Runs before this process touches
-    the GPU, so the spawned workers never inherit a GPU context."""
+    the GPU, so the spawned workers never inherit a GPU context.  `procs` defaults to the GPU
+    box's CPU share per GPU (16): the pool allots that many host CPUs to a one-GPU job although
+    os.cpu_count() shows the whole machine, so the whole-host figure is reported as a per-core
+    extrapolation (the workers share nothing, so the rate scales with cores), not measured."""
     import multiprocessing as mp
-    import platform
     jobs = [(seconds, schedule, alpha, L, 11 + i) for i in range(procs)]
     if procs == 1:
         res = [_cpu_worker(jobs[0])]
@@ -211,19 +251,17 @@ def cpu_baseline(seconds, schedule, alpha, L, procs):
             res = pool.map(_cpu_worker, jobs)
     done = sum(d for d, _ in res)
     el = max(e for _, e in res)
-    cpu = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
+    h = host_info()
     what = {"layered": "layered float32", "flooding": "flooding float32",
             "flooding64": "flooding float64 (the reference's algorithm and arithmetic)"}[schedule]
+    per_core = done / el / procs
     return {"value": round(done / el, 3), "unit": "codeblocks/s", "cores": procs, "kind": "port",
             "sample": f"{done} BG1 Zc=384 codeblocks (8 per call) over {procs} processes, "
                       f"{what} NMS alpha={alpha} L={L}, snr -3 dB (all iterations), "
-                      f"oracle/ldpc_oracle.py numpy, {el:.1f} s; host {cpu}, "
-                      f"os.cpu_count()={os.cpu_count()}",
+                      f"oracle/ldpc_oracle.py numpy, {el:.1f} s; {_host_cpu()}",
+            "host": h, "per_core": round(per_core, 3),
+            "all_physical_cores_extrapolated": (round(per_core * h["physical_cores"], 1)
+                                                if h["physical_cores"] else None),
             "reference_measured_in_build_container": {
                 "value": 0.073, "unit": "codeblocks/s", "cores": 1,
                 "note": "py5gphy nr_decode_ldpc itself, 13.2-14.1 s per BG1 Zc=384 CB at L=8 "
@@ -403,68 +441,33 @@ def valu_line(edges, ms):
             "frac": round(t / VALU_PEAK_TLANE, 4), "bound": "valu"}
 
 
-def bench_config4(torch, dist, world, dev, rank, steps):
-    """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
-    (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
-    GPU chain (encode -> rate match -> BPSK+AWGN), OMS beta=0.5, L=8.  The timed step is the
-    receive side: the 12 groups' rate recovery in ONE launch (ldpc5g_sch_raterecover_multi_plan,
-    per-group geometry uploaded once) + the mixed-Zc decode (ldpc5g_decode_ms_mixed_plan, plan built once).  The decode's
-    lane-op roofline is reported twice: on the algorithmic count (all rows x each codeblock's
-    iterations) and on the work the kernel executes (live rows only — a row whose extension column
-    was never transmitted is skipped — x the iterations of the slowest codeblock of each workgroup,
-    which every codeblock packed into that workgroup runs)."""
-    import numpy as np
+def _config4_groups(rng):
+    """BASELINE config 4's 12 (Zc, BG) groups with their random (Qm, rv, E in [K, 1.6N])."""
     from python_5gtoolbox_amd.ldpc_info import code_dims
-    from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
-    from python_5gtoolbox_amd.sch import SchRaterecoverPlan, cfg_from_codeblocks, sch_ratematch_batch
-    rng = np.random.default_rng(404 + rank)
-    g = torch.Generator(device=dev)
-    g.manual_seed(404 + rank)
-    n_per, snr = 341, 1.0
-    cfgs, llrs, info_bits, rr_bytes, meta = [], [], 0, 0, []
+    out = []
     for Zc in (12, 40, 72, 176, 208, 384):
         for bg in (1, 2):
             K, N, _ = code_dims(bg, Zc)
             Qm = int(rng.choice([2, 4, 6, 8]))
             rv = int(rng.integers(0, 4))
             E = Qm * int(rng.integers(-(-K // Qm), int(1.6 * N) // Qm + 1))
-            cfg = cfg_from_codeblocks(n_per, K, K, Zc, bg, Qm, n_per * E, 1, rv)
-            ck = torch.randint(0, 2, (n_per, K), dtype=torch.int8, device=dev, generator=g)
-            gs = sch_ratematch_batch(ck, cfg, 1)
-            sigma = 10 ** (-snr / 20)
-            y = (1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g)
-            llrs.append((2 * y / sigma ** 2).reshape(-1))
-            cfgs.append(cfg)
-            rr_bytes += n_per * (4 * E + 4 * N)   # LLRs in, rate-recovered row out (float32)
-            meta.append((bg, Zc, K, N))
-            info_bits += n_per * K
-    rrp = SchRaterecoverPlan(cfgs, dev)   # geometry validated and uploaded once
-    lay = rrp.lay
-    llr = torch.zeros((len(cfgs), lay["max_E"]), dtype=torch.float32, device=dev)
-    for t_, x in enumerate(llrs):
-        llr[t_, :x.numel()] = x
-    del llrs
-    dn = rrp(llr, torch.empty((lay["dn"],), dtype=torch.float32, device=dev))
-    groups = [(bg, Zc, dn[r[2]:r[2] + r[1] * N].view(r[1], N)) for (bg, Zc, K, N), r in zip(meta, lay["rows"])]
-    mb = MixedBatch(groups, flat=dn)
-    B = mb.B
+            out.append((bg, Zc, K, N, Qm, rv, E))
+    return out
 
-    def step():   # rate recovery (one launch) + decode (<= 3 launches), all on the GPU
-        rrp(llr, dn)
-        mb.decode(8, 1.0, 0.5, "layered", True)
-    wall, ev = timed(torch, dist, world, step, steps, 2)
-    _, st, it = mb.decode(8, 1.0, 0.5, "layered", True)
-    rr_ms = ev_ms(torch, lambda: rrp(llr, dn))
-    dec_ms = ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, "layered", True))
-    # work accounting on the host: the plan's workgroups (per (bgn, Zc) group: a partial workgroup
-    # of n % G codeblocks first, then full ones of G = floor(768 / Zc) — ldpc5g_capi.hip build_plan)
-    its = it.cpu().numpy().astype(np.int64)
-    dnh = dn.cpu().numpy()
+
+C4_N_PER, C4_SNR, C4_SEED = 341, 1.0, 404
+
+
+def _c4_executed(its, dnh, meta, rows, Gw_of):
+    """(algorithmic, executed) edge-updates of a config-4 decode and the per-codeblock iterations
+    its workgroups run: the plan's workgroups (per (bgn, Zc) group a partial workgroup of n % G
+    codeblocks first, then full ones of G = Gw_of(Zc) — ldpc5g_capi.hip build_plan)."""
+    import numpy as np
     alg_edges = exe_edges = wg_iters = 0
     cb0 = 0
-    for (bg, Zc, K, N), r in zip(meta, lay["rows"]):
+    for (bg, Zc, K, N), r in zip(meta, rows):
         n = r[1]
-        Gw = 768 // Zc
+        Gw = Gw_of(Zc)
         rows_cb = dnh[r[2]:r[2] + n * N].reshape(n, N)
         # extension column c of the transmitted row layout: columns 2..(N/Zc+1) of the full graph;
         # ext row i (>= 4) <-> full column KB + i <-> transmitted column KB + i - 2
@@ -486,28 +489,149 @@ def bench_config4(torch, dist, world, dev, rank, steps):
             wg_iters += int(its[cb0 + w0:cb0 + w1].max()) * (w1 - w0)
         alg_edges += int(its[cb0:cb0 + n].sum()) * sum(row_deg) * Zc
         cb0 += n
-    mean_it = float(its.mean())
-    dec_alg = valu_line(alg_edges, dec_ms)
-    dec_exe = valu_line(exe_edges, dec_ms)
+    return alg_edges, exe_edges, wg_iters
+
+
+def _cpu_worker_c4(job):
+    """One host process of config 4's reference-precision CPU baseline: the oracle's float64 rate
+    recovery (raterecover, nr_ldpc_raterecover.py:6-65) + float64 flooding OMS beta=0.5 L=8
+    (decode_ldpc, nr_ldpc_decode.py:51-143) over `n` codeblocks of each of the 12 groups, repeated
+    until `seconds` have passed."""
+    seconds, seed, n = job
+    import numpy as np
+    from oracle import ldpc_oracle as O
+    rng = np.random.default_rng(C4_SEED)   # the GPU line's groups (rank 0)
+    groups = _config4_groups(rng)
+    rng = np.random.default_rng(seed)
+    work = []
+    for bg, Zc, K, N, Qm, rv, E in groups:
+        k0 = O.get_k0(N, bg, rv, Zc)
+        ck = rng.integers(0, 2, (n, K)).astype(np.int8)
+        dn = O.encode(ck, bg)
+        sigma = 10 ** (-C4_SNR / 20)
+        fe = [2 * ((1 - 2 * O.ratematch(d, N, E, k0, Qm).astype(np.float64)) + sigma * rng.normal(size=E)) / sigma ** 2
+              for d in dn]
+        work.append((bg, Zc, K, N, Qm, k0, fe))
+    done, t0 = 0, time.perf_counter()
+    while True:
+        for bg, Zc, K, N, Qm, k0, fe in work:
+            rows = np.stack([O.raterecover(x, N, N, k0, Qm, Zc, K, K) for x in fe])
+            O.decode_flooding(rows, Zc, bg, 8, 1.0, 0.5, np.float64)
+            done += len(fe)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done, el
+
+
+def cpu_baseline_c4(seconds, procs, n=2):
+    """config 4 at the reference's precision on the host (kind "port"), procs processes."""
+    import multiprocessing as mp
+    jobs = [(seconds, 41 + i, n) for i in range(procs)]
+    if procs == 1:
+        res = [_cpu_worker_c4(jobs[0])]
+    else:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker_c4, jobs)
+    done = sum(d for d, _ in res)
+    el = max(e for _, e in res)
+    return {"value": round(done / el, 3), "unit": "codeblocks/s", "cores": procs, "kind": "port",
+            "sample": f"{done} codeblocks ({n} of each of the 12 (Zc, BG) groups per round) over "
+                      f"{procs} processes: oracle float64 raterecover + float64 flooding OMS "
+                      f"beta=0.5 L=8 (the reference's algorithm and arithmetic), {el:.1f} s; "
+                      f"{_host_cpu()}"}
+
+
+def bench_config4(torch, dist, world, dev, rank, steps, cpu_c4=None):
+    """BASELINE config 4: mixed-Zc batch {12,40,72,176,208,384} x BG1/BG2, 341 codeblocks per
+    (Zc, BG) = 4092, each group rate-matched with its own random (Qm, rv, E in [K, 1.6N]) on the
+    GPU chain (encode -> rate match -> BPSK+AWGN), OMS beta=0.5, L=8.  The timed step is the
+    receive side: the 12 groups' rate recovery in ONE launch (ldpc5g_sch_raterecover_multi_plan,
+    per-group geometry uploaded once) + the mixed-Zc decode (ldpc5g_decode_ms_mixed_plan, plan
+    built once).  Two lines: the float32 layered perf kernel (top level), and
+    `reference_precision`: the reference's own arithmetic — float64 LLRs rate-recovered into
+    float64 rows (nr_ldpc_raterecover.py:62) and decoded by float64 flooding (nr_dlsch_decode.py:91
+    -> nr_ldpc_decode.py:51-143), bit-identical to it, with a same-algorithm CPU baseline.  Each
+    decode's lane-op roofline is reported twice: on the algorithmic count (all rows x each
+    codeblock's iterations) and on the work the kernel executes (live rows only — a row whose
+    extension column was never transmitted is skipped — x the iterations of the slowest codeblock
+    of each workgroup, which every codeblock packed into that workgroup runs)."""
+    import numpy as np
+    from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
+    from python_5gtoolbox_amd.sch import SchRaterecoverPlan, cfg_from_codeblocks, sch_ratematch_batch
+    rng = np.random.default_rng(C4_SEED + rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(C4_SEED + rank)
+    n_per, snr = C4_N_PER, C4_SNR
+    cfgs, llrs, info_bits, meta = [], [], 0, []
+    ebytes = nbytes = 0
+    for bg, Zc, K, N, Qm, rv, E in _config4_groups(rng):
+        cfg = cfg_from_codeblocks(n_per, K, K, Zc, bg, Qm, n_per * E, 1, rv)
+        ck = torch.randint(0, 2, (n_per, K), dtype=torch.int8, device=dev, generator=g)
+        gs = sch_ratematch_batch(ck, cfg, 1)
+        sigma = 10 ** (-snr / 20)
+        y = (1 - 2 * gs.float()) + sigma * torch.randn(gs.shape, device=dev, generator=g)
+        llrs.append((2 * y / sigma ** 2).reshape(-1))
+        cfgs.append(cfg)
+        ebytes += n_per * E
+        nbytes += n_per * N
+        meta.append((bg, Zc, K, N))
+        info_bits += n_per * K
+    rrp = SchRaterecoverPlan(cfgs, dev)   # geometry validated and uploaded once
+    lay = rrp.lay
+    llr = torch.zeros((len(cfgs), lay["max_E"]), dtype=torch.float32, device=dev)
+    for t_, x in enumerate(llrs):
+        llr[t_, :x.numel()] = x
+    del llrs
+
+    def line(dt, schedule, Gw_of):
+        x = llr if dt == torch.float32 else llr.to(dt)
+        dn = rrp(x, torch.empty((lay["dn"],), dtype=dt, device=dev))
+        groups = [(bg, Zc, dn[r[2]:r[2] + r[1] * N].view(r[1], N))
+                  for (bg, Zc, K, N), r in zip(meta, lay["rows"])]
+        mb = MixedBatch(groups, flat=dn)
+        B = mb.B
+
+        def step():   # rate recovery (one launch) + decode (<= 3 launches), all on the GPU
+            rrp(x, dn)
+            mb.decode(8, 1.0, 0.5, schedule, True)
+        wall, ev = timed(torch, dist, world, step, steps, 2)
+        _, st, it = mb.decode(8, 1.0, 0.5, schedule, True)
+        rr_ms = ev_ms(torch, lambda: rrp(x, dn))
+        dec_ms = ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, schedule, True))
+        its = it.cpu().numpy().astype(np.int64)
+        alg_edges, exe_edges, wg_iters = _c4_executed(its, dn.cpu().numpy(), meta, lay["rows"], Gw_of)
+        dec_alg = valu_line(alg_edges, dec_ms)
+        dec_exe = valu_line(exe_edges, dec_ms)
+        es = x.element_size()
+        return {"codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
+                "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
+                "ms_per_step": round(wall / steps * 1e3, 4),
+                "mean_iterations": round(float(its.mean()), 3),
+                "converged_frac": round(st.float().mean().item(), 4),
+                "kernels": {
+                    "decode": {**dec_alg, "frac_executed": dec_exe["frac"],
+                               "achieved_executed": dec_exe["achieved"], "edge_updates_executed": exe_edges,
+                               "iterations_run_per_codeblock": round(wg_iters / max(B, 1), 3),
+                               "note": "frac: 13 lane-ops x (every row's edges x each codeblock's "
+                                       "iterations); frac_executed: the same over the work the kernel "
+                                       "runs — live rows only x the slowest codeblock's iterations of "
+                                       "each workgroup, for every codeblock packed in it"},
+                    "raterecover": {**hbm_line(es * (ebytes + nbytes), rr_ms),
+                                    "note": f"all 12 groups in ONE launch ({x.dtype} in, {x.dtype} rows "
+                                            f"out: {es}E + {es}N bytes per codeblock), inside the timed step"}}}
+    perf = line(torch.float32, "layered", lambda Zc: 768 // Zc)
+    ref = line(torch.float64, "flooding", lambda Zc: max(1, 384 // Zc))
+    ref.update({"dtype": "f64", "schedule": "flooding",
+                "what": "float64 LLRs -> float64 rate recovery (one launch) -> float64 flooding OMS "
+                        "beta=0.5 L=8 (LDPC5G_RATE_MATCHED): the reference's own arithmetic "
+                        "(DLSCHDecode: nr_dlsch_decode.py:62-91), bit-identical to it",
+                "cpu_baseline": cpu_c4})
+    if cpu_c4:
+        ref["vs_cpu_baseline"] = round(ref["codeblocks_per_s"] / cpu_c4["value"], 1)
     return {"workload": "BASELINE config 4: 12 (Zc, BG) groups x 341 CBs, random (Qm, rv, E), "
                         "GPU rate match, snr 1 dB, timed step = rate recovery (one launch) + "
-                        "layered OMS beta=0.5 L=8 decode (LDPC5G_RATE_MATCHED)",
-            "codeblocks_per_gpu": B, "codeblocks_per_s": round(B * world * steps / wall, 1),
-            "info_gbit_s": round(info_bits * world * steps / wall / 1e9, 3),
-            "ms_per_step": round(wall / steps * 1e3, 4),
-            "mean_iterations": round(mean_it, 3),
-            "converged_frac": round(st.float().mean().item(), 4),
-            "kernels": {
-                "decode": {**dec_alg, "frac_executed": dec_exe["frac"],
-                           "achieved_executed": dec_exe["achieved"], "edge_updates_executed": exe_edges,
-                           "iterations_run_per_codeblock": round(wg_iters / max(B, 1), 3),
-                           "note": "frac: 13 lane-ops x (every row's edges x each codeblock's "
-                                   "iterations); frac_executed: the same over the work the kernel "
-                                   "runs — live rows only x the slowest codeblock's iterations of "
-                                   "each workgroup, for every codeblock packed in it"},
-                "raterecover": {**hbm_line(rr_bytes, rr_ms),
-                                "note": "all 12 groups in ONE launch (float32 in, float32 rows out: "
-                                        "4E + 4N bytes per codeblock), inside the timed step"}}}
+                        "layered OMS beta=0.5 L=8 decode (LDPC5G_RATE_MATCHED); float32 perf mode",
+            "dtype": "f32", "schedule": "layered", **perf, "reference_precision": ref}
 
 
 # base-graph row degrees (TS 38.212 Tables 5.3.2-2/-3: edges per base row)
@@ -517,20 +641,80 @@ _ROW_DEG = {1: [19, 19, 19, 19, 3, 8, 9, 7, 10, 9, 7, 8, 7, 6, 7, 7, 6, 6, 6, 6,
                 3, 5, 3, 4, 4, 4, 4, 4, 3, 4, 4, 4, 4]}
 
 
-def bench_config5(torch, dist, world, dev, rank, steps, T=32):
+C5 = dict(A=1081512, Qm=8, R=948, NL=4, rv=0, G=8 * 4 * 36036)
+
+
+def _cpu_worker_c5(job):
+    """One host process of config 5's reference-precision CPU baseline: the oracle DL-SCH receive
+    chain at 30 dB — 256QAM soft demodulation of complex128 symbols (float32 LLRs, as
+    nr_Demodulation.py returns them) + descrambling, float64 rate recovery of the 129 codeblocks,
+    float64 flooding NMS alpha=0.75 L=8, TB reassembly + CRCs — on one transport block, repeated
+    until `seconds` have passed."""
+    seconds, seed = job
+    import numpy as np
+    from oracle import ldpc_oracle as O
+    rng = np.random.default_rng(seed)
+    c = C5
+    p = O.sch_params(c["A"], c["Qm"], c["R"], c["NL"], c["rv"], c["A"], c["G"])
+    tb = rng.integers(0, 2, c["A"]).astype(np.int8)
+    cinit = 7 + seed
+    g = O.sch_encode(tb, c["A"], c["Qm"], c["R"], c["NL"], c["rv"], c["A"], c["G"])
+    sym = O.modulate(g ^ O.prbs(cinit, g.size), c["Qm"]).astype(np.complex128)
+    nvar = 10 ** (-30.0 / 10)
+    y = sym + (rng.normal(size=sym.size) + 1j * rng.normal(size=sym.size)) * (nvar / 2) ** 0.5
+    nv = np.full(sym.size, nvar, np.float32)
+    done, ok, t0 = 0, 0, time.perf_counter()
+    while True:
+        llr = O.descramble(O.demodulate(y, nv, c["Qm"]), cinit)
+        rows = O.sch_raterecover(llr, p)
+        ck, _, _ = O.decode_flooding(rows, p["Zc"], p["bgn"], 8, 0.75, 0.0, np.float64)
+        tb_ok, blk, _ = O.sch_tb_check(ck, p)
+        done += 1
+        ok += bool(tb_ok) and np.array_equal(blk[:c["A"]], tb)
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done, el, ok
+
+
+def cpu_baseline_c5(seconds, procs):
+    """config 5 at the reference's precision on the host (kind "port"), procs processes."""
+    import multiprocessing as mp
+    jobs = [(seconds, 51 + i) for i in range(procs)]
+    if procs == 1:
+        res = [_cpu_worker_c5(jobs[0])]
+    else:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker_c5, jobs)
+    done = sum(r[0] for r in res)
+    el = max(r[1] for r in res)
+    return {"value": round(done / el, 4), "unit": "TB/s", "cores": procs, "kind": "port",
+            "codeblocks_per_s": round(done * 129 / el, 2),
+            "tb_crc_ok": f"{sum(r[2] for r in res)}/{done}",
+            "sample": f"{done} transport blocks (TBS {C5['A']}, 129 BG1 Zc=384 codeblocks, 256QAM, "
+                      f"30 dB) over {procs} processes: oracle demodulation (complex128 -> float32 "
+                      f"LLRs) + descrambling + float64 rate recovery + float64 flooding NMS "
+                      f"alpha=0.75 L=8 + TB CRC (the reference's algorithm and arithmetic), "
+                      f"{el:.1f} s; {_host_cpu()}"}
+
+
+def bench_config5(torch, dist, world, dev, rank, steps, T=32, cpu_c5=None):
     """BASELINE config 5: PDSCH 273 PRB 256QAM MCS27 4 layers TB stream (TBS 1,081,512 ->
     129 BG1 Zc=384 codeblocks per TB, G = 8*4*36036), T TBs per GPU, every step on the GPU:
     TX = ldpc5g_sch_encode + scrambling/256QAM mapping; RX = soft demodulation/descrambling +
-    ldpc5g_sch_decode (rate recovery, layered NMS L=8, CB/TB CRCs).  Channel: complex AWGN on the
-    symbols (outside the timed regions), at 30 dB (easy: ~3 iterations) and at the threshold point
-    (the highest SNR of a list at which the decoder needs >= 6 mean iterations, the same SNR on
-    every rank), each with its TB CRC pass rate; per-kernel split + rooflines at the threshold."""
+    ldpc5g_sch_decode (rate recovery, decode, CB/TB CRCs).  Two RX lines: the perf mode (complex64
+    symbols, float32 rate recovery, layered NMS L=8: the top level) and `reference_precision`
+    (DLSCHDecode's own arithmetic: complex128 symbols demodulated to float32 LLRs as
+    nr_Demodulation.py does, float64 rate recovery, float64 flooding NMS L=8 — bit-identical to
+    it), each with a per-kernel split.  Channel: complex AWGN on the symbols (outside the timed
+    regions), at 30 dB (easy: ~3 iterations) and at the threshold point (the highest SNR of a list
+    at which the layered decoder needs >= 6 mean iterations, the same SNR on every rank), each
+    with its TB CRC pass rate; per-kernel split + rooflines at the threshold."""
     from python_5gtoolbox_amd import phy
     from python_5gtoolbox_amd.nr_ldpc_decode import nr_decode_ldpc_batch
     from python_5gtoolbox_amd.sch import SchWorkspace, sch_config, sch_decode_batch, \
         sch_encode_batch, sch_raterecover_batch, sch_tb_check_batch
     from python_5gtoolbox_amd.shard import decode_tbs_sharded
-    A, Qm, R, NL, rv, G = 1081512, 8, 948, 4, 0, 8 * 4 * 36036
+    A, Qm, R, NL, rv, G = (C5[k] for k in ("A", "Qm", "R", "NL", "rv", "G"))
     cfg = sch_config(A, Qm, R, NL, rv, A, G)
     g = torch.Generator(device=dev)
     g.manual_seed(505 + rank)
@@ -552,30 +736,34 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
         noise = torch.complex(torch.randn(sym.shape, device=dev, generator=g),
                               torch.randn(sym.shape, device=dev, generator=g)) * (nvar / 2) ** 0.5
         cur["y"] = (sym + noise).contiguous()
+        cur["y128"] = cur["y"].to(torch.complex128)
         del noise
         cur["nv"] = torch.full(sym.shape, nvar, dtype=torch.float32, device=dev)
 
     last = {}
+    MODES = {"perf": ("y", "layered", torch.float32), "ref": ("y128", "flooding", torch.float64)}
 
-    def rx_local(y_local):
+    def rx_local(y_local, mode):
+        _, sched, dnt = MODES[mode]
         phy.demod_descramble(y_local, cur["nv"], Qm, cinit, out=llr)
-        r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered", ws=ws)
+        r = sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, sched, dn_dtype=dnt, ws=ws)
         last["r"] = r
         return r.tb_ok, r.tbblk
     tm = {}
     gather = world == 1 or dist.get_backend() == "nccl"   # gloo cannot gather device tensors
 
-    def rx():
+    def rx(mode):
         # this rank's TBs (round robin over T*world) -> records -> ONE RCCL gather to rank 0
+        y = cur[MODES[mode][0]]
         if gather:
-            return decode_tbs_sharded(cur["y"], cfg, 8, T_total=T * world, decode_fn=rx_local,
-                                      timing=tm)
-        return rx_local(cur["y"])
+            return decode_tbs_sharded(y, cfg, 8, T_total=T * world,
+                                      decode_fn=lambda yl: rx_local(yl, mode), timing=tm)
+        return rx_local(y, mode)
 
-    def rx_line(snr):
+    def rx_line(snr, mode="perf"):
         channel(snr)
-        wr, _ = timed(torch, dist, world, rx, steps, 2)
-        res = rx()
+        wr, _ = timed(torch, dist, world, lambda: rx(mode), steps, 2)
+        res = rx(mode)
         r = last["r"]
         ok = r.tb_ok.bool()
         # TBs that pass their CRC carry the transmitted bits
@@ -591,13 +779,44 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
                 "tb_bits_match_where_crc_ok": good,
                 "mean_iterations": round(r.iters.float().mean().item(), 3)}
 
+    def split(mode):
+        """per-kernel split of the RX step at the current channel (event-timed, the same calls
+        rx makes), with rooflines"""
+        ykey, sched, dnt = MODES[mode]
+        y = cur[ykey]
+        t_demod = ev_ms(torch, lambda: phy.demod_descramble(y, cur["nv"], Qm, cinit, out=llr))
+        dn = sch_raterecover_batch(llr, cfg, None, dnt, ws)
+        t_rr = ev_ms(torch, lambda: sch_raterecover_batch(llr, cfg, None, dnt, ws))
+        dec_out = (ws.dec_ck, ws.status, ws.iters)
+        t_dec = ev_ms(torch, lambda: nr_decode_ldpc_batch(dn, cfg.Zc, cfg.bgn, 8, "min-sum", 0.75, 0.0,
+                                                          sched, out=dec_out, rate_matched=True))
+        t_chk = ev_ms(torch, lambda: sch_tb_check_batch(ws.dec_ck, cfg, T, ws))
+        n_sym, ncb = T * (G // Qm), T * cfg.C
+        it_mean = ws.iters.float().mean().item()
+        ys, es = y.element_size(), dn.element_size()
+        out = {
+            "demod_descramble": {**hbm_line(n_sym * (ys + 4) + T * G * 4 + 2 * T * G // 8, t_demod),
+                                 "note": f"{y.dtype} symbol + float32 noise variance in, Qm float32 "
+                                         "LLRs out, packed scrambling words written + read (PRBS "
+                                         "kernel included)"},
+            "raterecover": {**hbm_line(T * cfg.E_total * 4 + ncb * cfg.N * es, t_rr),
+                            "note": f"E float32 LLRs in, N {dn.dtype} rate-recovered LLRs out per CB"},
+            "decode": {**valu_line(ncb * 316 * cfg.Zc * it_mean, t_dec),
+                       "mean_iterations": round(it_mean, 3), "schedule": sched, "dtype": str(dn.dtype),
+                       "note": f"{sched}, LDPC5G_RATE_MATCHED (dead extension rows skipped: fewer "
+                               "edge-updates done than counted)"},
+            "tb_check": hbm_line(ncb * (cfg.K_apo + cfg.cbz), t_chk),
+        }
+        out["sum_ms"] = round(t_demod + t_rr + t_dec + t_chk, 4)
+        return out
+
     easy = rx_line(30.0)
     # threshold search (untimed): mean decoder iterations per candidate SNR, averaged over ranks
     cands = [29.0, 28.0, 27.5, 27.0, 26.5, 26.25, 26.0, 25.5, 25.0, 24.0]
     its = []
     for snr in cands:
         channel(snr)
-        rx_local(cur["y"])
+        rx_local(cur["y"], "perf")
         its.append(last["r"].iters.float().mean().item())
     if world > 1:
         v = torch.tensor(its, dtype=torch.float64,
@@ -606,34 +825,26 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
         its = (v / world).tolist()
     pick = next((c for c, m in zip(cands, its) if m >= 6.0), cands[-1])
     thr = rx_line(pick)
-    # per-kernel split at the threshold point (event-timed, the same calls rx makes)
-    y = cur["y"]
-    t_demod = ev_ms(torch, lambda: phy.demod_descramble(y, cur["nv"], Qm, cinit, out=llr))
-    dn = sch_raterecover_batch(llr, cfg, None, torch.float32, ws)
-    t_rr = ev_ms(torch, lambda: sch_raterecover_batch(llr, cfg, None, torch.float32, ws))
-    dec_out = (ws.dec_ck, ws.status, ws.iters)
-    t_dec = ev_ms(torch, lambda: nr_decode_ldpc_batch(dn, cfg.Zc, cfg.bgn, 8, "min-sum", 0.75, 0.0,
-                                                      "layered", out=dec_out, rate_matched=True))
-    t_chk = ev_ms(torch, lambda: sch_tb_check_batch(ws.dec_ck, cfg, T, ws))
-    n_sym, ncb = T * (G // Qm), T * cfg.C
-    it_mean = ws.iters.float().mean().item()
-    split = {
-        "demod_descramble": {**hbm_line(n_sym * (8 + 4) + T * G * 4 + 2 * T * G // 8, t_demod),
-                             "note": "complex64 symbol + float32 noise variance in, Qm float32 "
-                                     "LLRs out, packed scrambling words written + read (PRBS "
-                                     "kernel included)"},
-        "raterecover": {**hbm_line(T * cfg.E_total * 4 + ncb * cfg.N * 4, t_rr),
-                        "note": "E float32 LLRs in, N float32 rate-recovered LLRs out per CB"},
-        "decode": {**valu_line(ncb * 316 * cfg.Zc * it_mean, t_dec),
-                   "mean_iterations": round(it_mean, 3),
-                   "note": "layered, LDPC5G_RATE_MATCHED (dead extension rows skipped: fewer "
-                           "edge-updates done than counted)"},
-        "tb_check": hbm_line(ncb * (cfg.K_apo + cfg.cbz), t_chk),
-    }
-    split["sum_ms"] = round(t_demod + t_rr + t_dec + t_chk, 4)
+    thr_split = split("perf")
+    # the reference's precision: the same two channel points
+    ref_easy = rx_line(30.0, "ref")
+    ref_thr = rx_line(pick, "ref")
+    ref_split = split("ref")
+    ref = {**{k: ref_easy[k] for k in ("rx_tb_per_s", "rx_codeblocks_per_s", "rx_info_gbit_s",
+                                       "rx_ms_per_batch", "tb_crc_ok_frac", "mean_iterations")},
+           "snr_db": 30.0, "tb_bits_match": ref_easy["tb_bits_match_where_crc_ok"],
+           "dtype": "f64", "schedule": "flooding",
+           "what": "complex128 symbols -> float32 LLRs (nr_Demodulation.py) -> float64 rate recovery "
+                   "-> float64 flooding NMS alpha=0.75 L=8 -> CB/TB CRCs: DLSCHDecode's arithmetic "
+                   "(nr_dlsch_decode.py:62-106), bit-identical to it",
+           "threshold": {**ref_thr, "kernels": ref_split},
+           "cpu_baseline": cpu_c5}
+    if cpu_c5:
+        ref["vs_cpu_baseline"] = round(ref["rx_tb_per_s"] / cpu_c5["value"], 1)
     return {"workload": f"BASELINE config 5: {T} TBs/GPU x 129 CBs (TBS {A}, 256QAM, BG1 Zc=384, "
-                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN",
-            "tb_per_gpu": T, "codeblocks_per_tb": cfg.C,
+                        f"Ncb {cfg.Ncb}, E {cfg.E_lo}/{cfg.E_hi}), complex AWGN; RX float32 layered "
+                        "(perf mode)",
+            "tb_per_gpu": T, "codeblocks_per_tb": cfg.C, "dtype": "f32", "schedule": "layered",
             **{k: easy[k] for k in ("rx_tb_per_s", "rx_codeblocks_per_s", "rx_info_gbit_s",
                                     "rx_ms_per_batch", "tb_crc_ok_frac", "mean_iterations")},
             "snr_db": easy["snr_db"], "tb_bits_match": easy["tb_bits_match_where_crc_ok"],
@@ -642,7 +853,8 @@ def bench_config5(torch, dist, world, dev, rank, steps, T=32):
             "tx_ms_per_batch": round(wt / steps * 1e3, 4),
             "threshold": {**thr, "search": {"snr_db": cands,
                                            "mean_iterations": [round(m, 3) for m in its]},
-                          "kernels": split},
+                          "kernels": thr_split},
+            "reference_precision": ref,
             "gather": ({"what": "TB round robin over ranks; (tb_ok, tbblk) packed into "
                                 f"{tm.get('gather_bytes', 0) // max(world, 1) // max(T, 1)}-B records, "
                                 "ONE dist.gather (RCCL) to rank 0, unpacked there — inside rx",
@@ -796,7 +1008,7 @@ def main():
         sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}\n")
         sys.exit(2)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cpu_res = cpu64 = None
+    cpu_res = cpu64 = cpu_c4 = cpu_c5 = None
     if rank == 0 and args.cpu_seconds > 0:   # before any GPU initialisation
         procs = args.cpu_procs or min(16, os.cpu_count() or 1)
         seconds = args.cpu_seconds
@@ -808,6 +1020,9 @@ def main():
         cpu64 = cpu_baseline(seconds, "flooding64", args.alpha, args.L, procs)
         if not args.no_perf or args.headline == "layered":
             cpu_res = cpu_baseline(seconds, "layered", args.alpha, args.L, procs)
+        if not args.no_extras:   # configs 4 / 5 at the reference's precision, shorter samples
+            cpu_c4 = cpu_baseline_c4(min(seconds, 8.0), procs)
+            cpu_c5 = cpu_baseline_c5(min(seconds, 10.0), procs)
     import torch
     import torch.distributed as dist
     ndev = torch.cuda.device_count()
@@ -926,19 +1141,25 @@ def main():
         ex["config1_per_codeblock"] = bench_config1(rank)
         ex["dlsch_caller_shape"] = bench_dlsch_caller(rank)
         ex["single_codeblock_latency"] = bench_single_cb(torch, rank)
-        tm = {}
         from python_5gtoolbox_amd.shard import decode_codeblocks_sharded
         if world == 1 or dist.get_backend() == "nccl":   # gloo cannot gather device tensors
-            for _ in range(2):   # second run timed (first allocates)
-                decode_codeblocks_sharded(llr, ZC, BG, args.L, args.alpha, 0.0, "layered",
-                                          n_total=B * world, timing=tm)
-        if tm:
+            llr64 = llr.double()
+            g_lines = {}
+            for name, x, sched in (("reference_precision", llr64, "flooding"), ("perf_mode", llr, "layered")):
+                tm = {}
+                for _ in range(2):   # second run timed (first allocates)
+                    decode_codeblocks_sharded(x, ZC, BG, args.L, args.alpha, 0.0, sched,
+                                              n_total=B * world, timing=tm)
+                g_lines[name] = {"schedule": sched, "dtype": "f64" if x is llr64 else "f32",
+                                 "gather_ms": round(tm["gather_s"] * 1e3, 3),
+                                 "decode_ms": round(tm["decode_s"] * 1e3, 3),
+                                 "gather_bytes": tm["gather_bytes"]}
+            del llr64
             ex["multi_gpu_gather"] = {
                 "what": "decode this rank's shard, pack info bits + status + iterations into "
-                        "1061-B records on the GPU, ONE dist.gather (RCCL) to rank 0, unpack there",
-                "gather_ms": round(tm["gather_s"] * 1e3, 3),
-                "decode_ms": round(tm["decode_s"] * 1e3, 3),
-                "gather_bytes": tm["gather_bytes"], "ranks": world}
+                        "1061-B records on the GPU, ONE dist.gather (RCCL) to rank 0, unpack there; "
+                        "decode_codeblocks_sharded's default is the reference's float64 flooding",
+                **g_lines["reference_precision"], "perf_mode": g_lines["perf_mode"], "ranks": world}
         # algo='BF' / 'BP' (nr_decode_ldpc's other two algorithms) on 1024 codeblocks of the
         # headline shape, float64 LLRs, L iterations (all run at -3 dB)
         Bb = min(B, 1024)
@@ -964,8 +1185,9 @@ def main():
                          "float64 sum-product flooding (_BP_process, nr_ldpc_decode.py:145-176), per-edge "
                          "messages in a device scratch")}
         del x64
-        ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2))
-        ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2))
+        ex["config4_mixed_zc"] = bench_config4(torch, dist, world, dev, rank, max(3, args.steps // 2), cpu_c4)
+        ex["config5_tb_stream"] = bench_config5(torch, dist, world, dev, rank, max(3, args.steps // 2),
+                                                cpu_c5=cpu_c5)
         res["extras"] = ex
 
     if rank == 0:

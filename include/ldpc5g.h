@@ -240,7 +240,9 @@ int ldpc5g_sch_ratematch(const int8_t* ck, const ldpc5g_sch_cfg_t* cfg, int32_t 
 
 /* Rate recovery (nr_ldpc_raterecover.py:6-65) of every codeblock + optional HARQ combining with
  * the previous decoder inputs (nr_dlsch_decode.py:73-88):
- *   llr [T][ldg] (llr_dtype) -> llr_dn [T*C][N] (dn_dtype); harq_in NULL or [T*C][N] dn_dtype.
+ *   llr [T][ldg] (llr_dtype) -> llr_dn [T*C][N] (dn_dtype); harq_in NULL or [T*C][N] dn_dtype,
+ *   either disjoint from llr_dn or llr_dn itself (in-place combining with the previous call's
+ *   output); a partial overlap is not supported.  (Every rate-recovery entry point below too.)
  * Computed in float64 like the reference (a float32 llr_dn is the float64 result rounded once). */
 int ldpc5g_sch_raterecover(const void* llr, int32_t llr_dtype, int64_t ldg,
                            const ldpc5g_sch_cfg_t* cfg, int32_t T, const void* harq_in,
@@ -358,6 +360,27 @@ const char* ldpc5g_version(void);
 /* Diagnostics: decoder workgroups that can be resident on one CU (HIP occupancy calculator) for
  * (bgn, llr_dtype, schedule).  No reference counterpart. */
 int ldpc5g_dec_blocks_per_cu(int32_t bgn, int32_t llr_dtype, int32_t schedule);
+
+/* ---- the multi-workgroup float64 decoder (few large codeblocks per call).
+ * ldpc5g_decode_ms / ldpc5g_decode_ms_host / ldpc5g_sch_decode with float64 flooding and at most
+ * ~24 codeblocks of Zc >= 64 (the per-codeblock drop-ins' shape) run each codeblock over W (9-18)
+ * workgroups, one per CU, that synchronise through global memory twice per iteration.  It assumes:
+ *   - co-residency: a codeblock's W workgroups run at the same time.  Workgroups take their
+ *     (codeblock, part) by arrival ticket, so one launch never waits on itself, and launches use at
+ *     most 7/8 of the device's CUs; but a kernel of another library or process that holds CUs
+ *     indefinitely (a persistent kernel) could keep parts from starting.  A barrier wait therefore
+ *     gives up after 4 s: the codeblock is returned with status 0 and iters -1 (never silently
+ *     wrong), the device's timeout count grows (below), and the library stays usable;
+ *   - serialisation: split launches of one device are chained by one hidden event (they share a
+ *     per-device sync area and scratch), so they run one after another whatever their streams;
+ *   - the first split launch on a device, and one needing more scratch, allocate (hipMalloc /
+ *     hipMemset / a device synchronisation, or an event wait + hipFree when growing): not capturable.
+ *     A stream in capture (hipStreamIsCapturing) never takes this path — such launches run the
+ *     one-workgroup-per-codeblock kernels instead (same results, bit for bit).
+ * ldpc5g_split_timeouts: the number of codeblocks of the current device whose split decode timed
+ * out since the process started (waits for the device's last split launch).  No reference
+ * counterpart. */
+int ldpc5g_split_timeouts(uint32_t* count);
 
 #ifdef __cplusplus
 }

@@ -22,7 +22,7 @@ EBGN, EZC, ESIZE, EHIP = -1, -2, -3, -4
 
 # every symbol include/ldpc5g.h declares: name -> (restype, argtypes)
 _c = ctypes
-OPTIONAL = {"ldpc5g_dec_blocks_per_cu"}
+OPTIONAL = {"ldpc5g_dec_blocks_per_cu", "ldpc5g_split_timeouts"}
 SIGNATURES = {
     "ldpc5g_find_ils": (_c.c_int, [_c.c_int32]),
     "ldpc5g_dec_blocks_per_cu": (_c.c_int, [_c.c_int32, _c.c_int32, _c.c_int32]),
@@ -115,6 +115,7 @@ SIGNATURES = {
     "ldpc5g_unpack_records": (_c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int32, _c.c_int64,
                                          _c.c_void_p, _c.c_int64, _c.c_void_p, _c.c_void_p,
                                          _c.c_int64, _c.c_void_p]),
+    "ldpc5g_split_timeouts": (_c.c_int, [_c.c_void_p]),
     "ldpc5g_last_error": (_c.c_char_p, []),
     "ldpc5g_version": (_c.c_char_p, []),
 }
@@ -260,3 +261,11 @@ def to_host(x, key):
     hout.copy_(x, non_blocking=True)
     t.cuda.current_stream().synchronize()
     return hout.numpy().copy()
+
+
+def split_timeouts():
+    """Codeblocks of the current device whose multi-workgroup float64 decode gave up waiting for
+    its parts to be co-resident (status 0, iters -1; include/ldpc5g.h ldpc5g_split_timeouts)."""
+    n = ctypes.c_uint32(0)
+    check(lib().ldpc5g_split_timeouts(ctypes.byref(n)))
+    return int(n.value)

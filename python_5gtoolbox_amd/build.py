@@ -9,6 +9,8 @@ Each csrc/*.hip translation unit is compiled to an object in parallel, then link
 python_5gtoolbox_amd/libldpc5g.so, which travels with the repo snapshot to the GPU box.
 """
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -39,11 +41,27 @@ def deps():
     return sources() + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "ldpc5g.h")]
 
 
-def _stamp():
-    """Everything besides the sources that decides the library's code: a library built with other
-    flags or for another arch (an A/B build into the default path) is never reused as the product."""
+def _digest(paths):
+    """{path: sha1 of its contents} (missing files map to None)."""
+    out = {}
+    for p in paths:
+        try:
+            with open(p, "rb") as f:
+                out[os.path.abspath(p)] = hashlib.sha1(f.read()).hexdigest()
+        except OSError:
+            out[os.path.abspath(p)] = None
+    return out
+
+
+def _stamp(dig=None):
+    """Everything that decides the library's code: flags and arch (a library built with other
+    flags or for another arch — an A/B build into the default path — is never reused as the
+    product) and the contents of every source, as they were when the build STARTED (a source
+    edited while the build ran leaves the library stale, not falsely up to date)."""
+    dig = dig if dig is not None else _digest(deps())
     return " ".join([HIPCC, ARCH, *FLAGS, os.environ.get("LDPC5G_EXTRA_FLAGS", ""),
-                     os.environ.get("LDPC5G_SLP", ""), *sorted(NO_SLP)])
+                     os.environ.get("LDPC5G_SLP", ""), *sorted(NO_SLP)]) + "\n" + \
+        json.dumps(sorted((os.path.relpath(k, ROOT), v) for k, v in dig.items()))
 
 
 def up_to_date():
@@ -51,29 +69,23 @@ def up_to_date():
         return False
     try:
         with open(LIB + ".stamp") as f:
-            if f.read() != _stamp():
-                return False
+            return f.read() == _stamp()
     except OSError:
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(d) <= t for d in deps())
 
 
 def _obj_fresh(obj, cmd):
-    """The object exists, was built by exactly `cmd`, and is newer than every file its
-    dependency list (hipcc -MMD) names."""
+    """The object exists, was built by exactly `cmd`, and every file its dependency list (hipcc
+    -MMD) names still has the contents it had when that compile started (.dig)."""
     try:
         with open(obj + ".cmd") as f:
             if f.read() != " ".join(cmd):
                 return False
-        with open(obj + ".d") as f:
-            text = f.read().replace("\\\n", " ")
-        t = os.path.getmtime(obj)
-    except OSError:
+        with open(obj + ".dig") as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
         return False
-    deps_ = text.split(":", 1)[1].split() if ":" in text else []
-    return bool(deps_) and all(os.path.getmtime(d) <= t for d in deps_ if os.path.exists(d)) and \
-        all(os.path.exists(d) for d in deps_)
+    return bool(rec) and _digest(rec) == rec
 
 
 def _compile(src, verbose, obj_dir=None, csrc=CSRC):
@@ -87,10 +99,26 @@ def _compile(src, verbose, obj_dir=None, csrc=CSRC):
         return obj
     if verbose:
         print(" ".join(cmd), flush=True)
+    _compile_recorded(cmd, obj)
+    return obj
+
+
+def _compile_recorded(cmd, obj):
+    """Run one compile and record its command and the contents of its dependencies as they
+    were when it started (every candidate file is hashed first; the -MMD list picks them)."""
+    before = _digest(deps())
     subprocess.run(cmd + ["-MMD", "-MF", obj + ".d"], check=True)
+    with open(obj + ".d") as f:
+        text = f.read().replace("\\\n", " ")
+    dl = text.split(":", 1)[1].split() if ":" in text else []
+    rec = {}
+    for d in dl:
+        a = os.path.abspath(d)
+        rec[a] = before[a] if a in before else _digest([a])[a]
+    with open(obj + ".dig", "w") as f:
+        json.dump(rec, f)
     with open(obj + ".cmd", "w") as f:
         f.write(" ".join(cmd))
-    return obj
 
 
 def build(force=False, verbose=True, csrc=None, out=None):
@@ -100,6 +128,7 @@ def build(force=False, verbose=True, csrc=None, out=None):
         if verbose:
             print("libldpc5g.so up to date")
         return LIB
+    stamp = _stamp()   # the sources as they are now: an edit during the build is not covered
     csrc = csrc or CSRC
     obj_dir = os.path.join(ROOT, "build", ("obj_alt_" + os.path.basename(lib_path)) if alt else "obj")
     os.makedirs(obj_dir, exist_ok=True)
@@ -113,7 +142,7 @@ def build(force=False, verbose=True, csrc=None, out=None):
     os.replace(lib_path + ".tmp", lib_path)
     if not alt:
         with open(LIB + ".stamp", "w") as f:
-            f.write(_stamp())
+            f.write(stamp)
     return lib_path
 
 
@@ -136,7 +165,8 @@ ASAN_SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=unde
 
 
 def _asan_stamp():
-    return " ".join([HIPCC, ARCH, *FLAGS, *ASAN_SAN, *sorted(NO_SLP)])
+    return " ".join([HIPCC, ARCH, *FLAGS, *ASAN_SAN, *sorted(NO_SLP)]) + "\n" + \
+        json.dumps(sorted((os.path.relpath(k, ROOT), v) for k, v in _digest(deps()).items()))
 
 
 def build_asan(force=False, verbose=False):
@@ -149,13 +179,13 @@ def build_asan(force=False, verbose=False):
     lazily by that test, not by the product build()."""
     out_dir = os.path.dirname(ASAN_LIB)
     stamp = ASAN_LIB + ".stamp"
+    want = _asan_stamp()   # the sources as they are when the build starts
     try:
         with open(stamp) as f:
-            same = f.read() == _asan_stamp()
+            same = f.read() == want
     except OSError:
         same = False
-    if not force and same and os.path.exists(ASAN_LIB) and \
-            all(os.path.getmtime(d) <= os.path.getmtime(ASAN_LIB) for d in deps()):
+    if not force and same and os.path.exists(ASAN_LIB):
         return ASAN_LIB
     os.makedirs(out_dir, exist_ok=True)
     san = list(ASAN_SAN)
@@ -170,9 +200,7 @@ def build_asan(force=False, verbose=False):
             return obj
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd + ["-MMD", "-MF", obj + ".d"], check=True)
-        with open(obj + ".cmd", "w") as f:
-            f.write(" ".join(cmd))
+        _compile_recorded(cmd, obj)
         return obj
     srcs = sources()
     with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
@@ -184,7 +212,7 @@ def build_asan(force=False, verbose=False):
     subprocess.run(link, check=True)
     os.replace(ASAN_LIB + ".tmp", ASAN_LIB)
     with open(stamp, "w") as f:
-        f.write(_asan_stamp())
+        f.write(want)
     return ASAN_LIB
 
 

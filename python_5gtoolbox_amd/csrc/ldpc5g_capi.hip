@@ -291,6 +291,12 @@ int ldpc5g_dec_blocks_per_cu(int32_t bgn, int32_t llr_dtype, int32_t schedule) {
 
 const char* ldpc5g_last_error(void) { return g_err.c_str(); }
 
+int ldpc5g_split_timeouts(uint32_t* count) {
+    clear_error();
+    if (!count) return fail(LDPC5G_ESIZE, "null count");
+    return split_timeouts(count);
+}
+
 int ldpc5g_find_ils(int32_t Zc) {
     int i = zc_index(Zc);
     return i < 0 ? 255 : kLdpcZcSet[i];

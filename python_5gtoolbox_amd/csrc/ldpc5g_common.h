@@ -186,6 +186,7 @@ int split_wanted(int bgn, int B, int Zc);
 int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,
                        int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta,
                        int pc, hipStream_t st);
+int split_timeouts(uint32_t* count);   // codeblocks whose split decode timed out (this device)
 int launch_bf(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
               int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc, hipStream_t st);
 int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

@@ -1,7 +1,12 @@
 // ldpc5g_dec.hip — flooding min-sum decoder instantiations (float64: the drop-in's bit-exact path;
 // float32 in ldpc5g_dec_f32.hip) and the decoder dispatch; the layered kernels live in ldpc5g_dec_l.hip.
 // Part of libldpc5g.so (MI355X, gfx950).
-#include "ldpc5g_dec_flood.h"
+#include "ldpc5g_dec_frame.h"
+
+// float64 Zc = 384 batches: the frame kernel (ldpc5g_dec_frame.h) instead of ldpc_flood_kernel
+#ifndef LDPC5G_FLOOD_FRAME
+#define LDPC5G_FLOOD_FRAME 1
+#endif
 
 namespace ldpc5g_impl {
 
@@ -18,7 +23,10 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
         return dead ? launch_dec_l_dead(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                     : launch_dec_l(bgn, (const float*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     // a few large float64 codeblocks (the per-codeblock drop-ins): each over several CUs
-    if (dtype == LDPC5G_F64 && split_wanted(bgn, B, Zc))
+    // (never while the stream is being captured: the split path may allocate on first use)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (dtype == LDPC5G_F64 && split_wanted(bgn, B, Zc) &&
+        (hipStreamIsCapturing(st, &cap) != hipSuccess || cap == hipStreamCaptureStatusNone))
         return launch_flood_split(bgn, (const double*)llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     // launches whose codeblocks fit 64 slots (one small codeblock per drop-in call): 16 parts
     const int G = std::min(dec_G(Zc, false), B);
@@ -27,6 +35,9 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
     if (dead) return launch_flood_dead(bgn, dtype, llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
+        if (LDPC5G_FLOOD_FRAME && Zc == kFrZ)
+            return bgn == 1 ? launch_frame_t<1>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st)
+                            : launch_frame_t<2>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
@@ -43,6 +54,8 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
     if (dead) return launch_flood_mixed_dead(bgn, dtype, llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st, zc384);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
+        if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
+            return launch_frame_t<1>(p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
         if (zc384 && bgn == 1)
             return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)

@@ -1,0 +1,859 @@
+// ldpc5g_dec_frame.h — float64 flooding min-sum decoder for lifting size Zc = 384 with per-row
+// thread frames (py5gphy/ldpc/nr_ldpc_decode.py:51-143, _min_sum_process :178-227).  Bit-identical
+// to the reference and to ldpc_flood_kernel (ldpc5g_dec_flood.h), whose two-phase data flow it
+// keeps: phase A forms every row's new compressed state from LQ_old, phase B sums the messages
+// into LQ in row-ascending order per column (Lr.sum(axis=0), :126).
+//
+// What changes is who sums what.  ldpc_flood_kernel adds each row's messages into the LDS image of
+// LQ with one barrier per group of column-disjoint rows, and columns 0 and 1 — 30 and 28 of BG1's 46
+// rows — make that 32 groups.  Here the thread that runs check node z' of row i is chosen per row
+// (its "frame"): a row with column 0 runs on half 0 with thread s = (z' + V(i,0)) mod Zc, a row
+// with column 1 but not 0 on half 1 with s = (z' + V(i,1)) mod Zc.  Then thread s of half 0 makes
+// the message of EVERY column-0 edge into column-0 entry s, and adds them in registers, in row
+// order, with no barrier; half 1 does column 1 the same way.  Rows with both columns keep their
+// state in LDS, where each half reads it in its own frame; when LDS is full (BG1: 3 rows), the
+// owner hands the other column's message over through the LDS image of columns 0 / 1, which is
+// dead during phase B.  The barrier groups only order columns >= 2: BG1 46 rows -> 18 groups
+// (32 before), BG2 42 -> 23 (28).
+#pragma once
+#include "ldpc5g_dec_flood.h"
+
+namespace ldpc5g_impl {
+namespace {
+
+constexpr int kFrZ = 384;
+constexpr int kFrThreads = 2 * kFrZ;
+constexpr int kFrColB = kFrZ * 8;          // one LQ column (float64) or hand-off slot
+constexpr int kFrRowB = kFrZ * (16 + 4);   // one LDS state row: (mA, mB) pairs + sign words
+constexpr int kFrFlagB = 64;
+// development knobs (tools/flood_dev): LDS-row state read one group ahead in phase B; the group
+// in which the LQ update's core LLRs are loaded (-1: at the start of phase B, else that many groups
+// after the last group with an LDS row); phase-B entry offsets from the wrap table
+#ifndef LDPC5G_FR_PREF
+#define LDPC5G_FR_PREF 0
+#endif
+#ifndef LDPC5G_FR_LFG
+#define LDPC5G_FR_LFG -1
+#endif
+#ifndef LDPC5G_FR_BTAB
+#define LDPC5G_FR_BTAB 0
+#endif
+// phase B pipelined: the messages of group g + 1 are formed (and its LDS-row state read) in section g,
+// right after group g's adds were issued, so the adds' LDS latency and the barrier overlap VALU work
+#ifndef LDPC5G_FR_PIPE
+#define LDPC5G_FR_PIPE 0
+#endif
+#ifndef LDPC5G_FR_EBAL
+#define LDPC5G_FR_EBAL 1
+#endif
+#ifndef LDPC5G_FR_PIPEA
+#define LDPC5G_FR_PIPEA 1
+#endif
+#ifndef LDPC5G_FR_ILV
+#define LDPC5G_FR_ILV 0
+#endif
+#ifndef LDPC5G_FR_BAL
+#define LDPC5G_FR_BAL 0
+#endif
+#ifndef LDPC5G_FR_USH
+#define LDPC5G_FR_USH 0
+#endif
+#ifndef LDPC5G_FR_LDS0
+#define LDPC5G_FR_LDS0 1
+#endif
+
+// Compile-time plan of the rows: LDS / VGPR state, owner half, frame, hand-offs, barrier groups.
+template <int BG>
+struct FramePlan {
+    int kc[2][64] = {};   // edge (index in the row) of column c, -1: none
+    bool lds[64] = {};    // state in LDS (either half can read it)
+    int lslot[64] = {};
+    int nls = 0;
+    int owner[64] = {};   // half that runs phase A (and the final pass) of row i
+    int fr[64] = {};      // frame column (0 / 1; -1: natural, thread s runs check node s)
+    int off[64] = {};     // V(i, fr) mod Zc: thread s runs check node (s - off) mod Zc
+    int slot[64] = {};    // VGPR state slot in the owner half
+    int nslot = 0;
+    int pw[64] = {}, ph[64] = {};   // VGPR sign word (rows of degree <= 12 share one: 16-bit fields)
+    int npw = 0;
+    int ho[64] = {};      // hand-off slot of a VGPR row with both columns 0 and 1, -1: none
+    int nho = 0, nspare = 0;
+    int first_row[32] = {};   // lowest row of column j >= 2 (writes 0 + r)
+    int xpos[64] = {}, xlist[2][64] = {}, nx[2] = {};   // extension rows per owner half
+    int ng = 0;
+    int gstart[65] = {};  // barrier groups: consecutive rows whose columns >= 2 are disjoint
+    int grp[64] = {};
+    int nlg = 1;          // most LDS rows in one group
+    int eh[64][20] = {};  // LDS rows: the half that adds edge k (column >= 2) in phase B
+    int st_b = 0, pk_b = 0, fl_b = 0, tbl_b = 0, sp_b = 0, bytes = 0;   // LDS layout
+    bool ok = true;
+
+    static constexpr int deg(int i) { return BGT<BG>::RS[i + 1] - BGT<BG>::RS[i]; }
+    static constexpr int fr_c2_(int i, int k) {   // core edges of columns >= 2 before edge k
+        int n = 0;
+        for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i] + k; ++e) n += BGT<BG>::COL[e] >= 2 && BGT<BG>::COL[e] < BGT<BG>::KC;
+        return n;
+    }
+    static constexpr int ncore2(int i) {   // core edges of columns >= 2
+        int n = 0;
+        for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i + 1]; ++e) n += BGT<BG>::COL[e] >= 2 && BGT<BG>::COL[e] < BGT<BG>::KC;
+        return n;
+    }
+    constexpr bool both(int i) const { return kc[0][i] >= 0 && kc[1][i] >= 0; }
+    constexpr int hb(int b) const { return b < 2 ? b * kFrColB : sp_b + (b - 2) * kFrColB; }
+
+    // the greedy split (decreasing degree onto the lighter half) as a bit mask of li[]
+    static constexpr int greedy_split(const int* li, int n, const int* ea0) {
+        int e[2] = {ea0[0], ea0[1]}, m = 0;
+        bool done[16] = {};
+        for (int c = 0; c < n; ++c) {
+            int best = -1;
+            for (int x = 0; x < n; ++x)
+                if (!done[x] && (best < 0 || deg(li[x]) > deg(li[best]))) best = x;
+            const int hh = e[0] <= e[1] ? 0 : 1;
+            done[best] = true, e[hh] += deg(li[best]), m |= hh << best;
+        }
+        return m;
+    }
+    constexpr FramePlan() {
+        using P = BGT<BG>;
+        const int MB = P::MB;
+        for (int i = 0; i < MB; ++i) {
+            kc[0][i] = kc[1][i] = -1;
+            ho[i] = -1;
+            for (int e = P::RS[i]; e < P::RS[i + 1]; ++e)
+                if (P::COL[e] < 2) kc[P::COL[e]][i] = e - P::RS[i];
+        }
+        gstart[0] = 0, ng = 1;
+        for (int i = 1, g0 = 0; i < MB; ++i) {
+            bool dis = true;
+            for (int a = g0; a < i && dis; ++a)
+                for (int e = P::RS[a]; e < P::RS[a + 1]; ++e)
+                    for (int f = P::RS[i]; f < P::RS[i + 1]; ++f)
+                        if (P::COL[e] == P::COL[f] && P::COL[e] >= 2 && P::COL[e] < P::KC) dis = false;
+            if (!dis) gstart[ng++] = i, g0 = i;
+        }
+        gstart[ng] = MB;
+        for (int g = 0; g < ng; ++g)
+            for (int i = gstart[g]; i < gstart[g + 1]; ++i) grp[i] = g;
+        // LDS rows: degree > 12 (split across the halves in phase B), then rows with both columns
+        // (no hand-off), then the longest rows while a half would hold more than 18 VGPR rows
+        const int fixed = P::KC * kFrColB + kFrFlagB + 2 * kFrZ * 4;
+        for (nspare = 0; nspare < 8; ++nspare) {
+            const int cap = (160 * 1024 - fixed - nspare * kFrColB) / kFrRowB;
+            for (int i = 0; i < MB; ++i) lds[i] = false;
+            nls = 0;
+            for (int pass = 0; pass < 3; ++pass)
+                for (;;) {
+                    if (nls >= cap || (pass == 2 && MB - nls <= 36)) break;
+                    int best = -1;
+                    for (int i = 0; i < MB; ++i) {
+                        const bool want = pass == 0 ? LDPC5G_FR_LDS0 && deg(i) > 12 : pass == 1 ? both(i) : true;
+                        if (!lds[i] && want && (best < 0 || deg(i) > deg(best))) best = i;
+                    }
+                    if (best < 0) break;
+                    lds[best] = true, ++nls;
+                }
+            nho = 0;
+            for (int i = 0; i < MB; ++i) nho += !lds[i] && both(i);
+            if (nho - 2 <= nspare) break;
+        }
+        if (nspare > 0 && nho - 2 < nspare) nspare = nho > 2 ? nho - 2 : 0;
+        for (int i = 0, n = 0; i < MB; ++i)
+            if (lds[i]) lslot[i] = n++;
+        // owners: a row with only column c runs on half c in frame c; rows with both (hand-off) or
+        // neither go where fewer VGPR rows are (then to the lighter half of their group)
+        int nv[2] = {}, ea[2] = {}, gl[2][64] = {};
+        for (int i = 0; i < MB; ++i) {
+            if (lds[i]) {
+                const int n = ncore2(i);
+                gl[0][grp[i]] += (n + 1) / 2, gl[1][grp[i]] += n / 2;
+                continue;
+            }
+            if ((kc[0][i] >= 0) == (kc[1][i] >= 0)) continue;
+            const int hh = kc[0][i] >= 0 ? 0 : 1;
+            owner[i] = hh, fr[i] = hh, ++nv[hh], ea[hh] += deg(i), gl[hh][grp[i]] += ncore2(i);
+        }
+        for (int i = 0, b = 0; i < MB; ++i) {
+            if (lds[i] || (kc[0][i] >= 0) != (kc[1][i] >= 0)) continue;
+            const int hh = nv[0] != nv[1] ? (nv[0] < nv[1] ? 0 : 1) : (gl[0][grp[i]] <= gl[1][grp[i]] ? 0 : 1);
+            owner[i] = hh, fr[i] = both(i) ? hh : -1, ++nv[hh], ea[hh] += deg(i), gl[hh][grp[i]] += ncore2(i);
+            if (both(i)) {
+                ho[i] = b++;
+                ok = ok && grp[i] >= 1;   // written before group 0's barrier, read after it
+            }
+        }
+        {   // LDS rows' phase A: the split of them that balances the halves' edges best
+            int li[16] = {}, n = 0;
+            for (int i = 0; i < MB; ++i)
+                if (lds[i]) li[n++] = i;
+            int best = 0, bd = 1 << 30;
+            for (int m = LDPC5G_FR_BAL ? 0 : greedy_split(li, n, ea); m < (1 << n); ++m) {
+                int e0 = ea[0], e1 = ea[1];
+                for (int x = 0; x < n; ++x) ((m >> x) & 1 ? e1 : e0) += deg(li[x]);
+                const int dd = e0 > e1 ? e0 - e1 : e1 - e0;
+                if (dd < bd) bd = dd, best = m;
+                if (!LDPC5G_FR_BAL) break;
+            }
+            for (int x = 0; x < n; ++x) owner[li[x]] = (best >> x) & 1, fr[li[x]] = -2, ea[(best >> x) & 1] += deg(li[x]);
+        }
+        for (int i = 0; i < MB; ++i) {
+            if (fr[i] == -2) fr[i] = -1;
+            off[i] = fr[i] < 0 ? 0 : zc_shift<BG, kFrZ>(P::RS[i] + kc[fr[i]][i]);
+        }
+        int ns[2] = {};
+        for (int i = 0; i < MB; ++i) slot[i] = lds[i] ? -1 : ns[owner[i]]++;
+        nslot = ns[0] > ns[1] ? ns[0] : ns[1];
+        for (int hh = 0; hh < 2; ++hh) {
+            int n = 0, open = -1;
+            for (int i = 0; i < MB; ++i) {
+                if (lds[i] || owner[i] != hh) continue;
+                if (deg(i) > 12) pw[i] = n++, ph[i] = 0;
+                else if (open >= 0) pw[i] = open, ph[i] = 2, open = -1;
+                else open = n, pw[i] = n++, ph[i] = 1;
+            }
+            npw = npw > n ? npw : n;
+        }
+        for (int i = 4; i < MB; ++i) xpos[i] = nx[owner[i]], xlist[owner[i]][nx[owner[i]]++] = i;
+        for (int j = 0; j < P::KC; ++j) {
+            first_row[j] = -1;
+            for (int i = 0; i < MB && first_row[j] < 0; ++i)
+                for (int e = P::RS[i]; e < P::RS[i + 1]; ++e)
+                    if (P::COL[e] == j) first_row[j] = i;
+        }
+        for (int g = 0; g < ng; ++g) {
+            int n = 0;
+            for (int i = gstart[g]; i < gstart[g + 1]; ++i) n += lds[i];
+            nlg = nlg > n ? nlg : n;
+            // LDS rows' adds go to the half with fewer adds in the group so far (VGPR rows fixed)
+            int ld[2] = {};
+            for (int i = gstart[g]; i < gstart[g + 1]; ++i)
+                if (!lds[i]) ld[owner[i]] += ncore2(i);
+            for (int i = gstart[g]; i < gstart[g + 1]; ++i)
+                for (int k = 0; lds[i] && k < deg(i); ++k) {
+                    const int j = P::COL[P::RS[i] + k];
+                    if (j < 2 || j >= P::KC) continue;
+                    const int hh = LDPC5G_FR_EBAL ? (ld[0] <= ld[1] ? 0 : 1) : fr_c2_(i, k) % 2;
+                    eh[i][k] = hh, ++ld[hh];
+                }
+        }
+        // every row holds column 0 or 1 in the 5G base graphs, or is a VGPR row (natural frame)
+        st_b = P::KC * kFrColB;
+        pk_b = st_b + nls * kFrZ * 16;
+        fl_b = pk_b + nls * kFrZ * 4;
+        tbl_b = fl_b + kFrFlagB;
+        sp_b = tbl_b + 2 * kFrZ * 4;
+        bytes = sp_b + nspare * kFrColB;
+        ok = ok && bytes <= 160 * 1024 && nho <= 2 + nspare && nslot <= 18;
+    }
+};
+template <int BG>
+constexpr FramePlan<BG> kFrPlan{};
+static_assert(kFrPlan<1>.ok && kFrPlan<2>.ok, "frame plan");
+
+// V(i, k) mod Zc of edge k of row i; the same relative to the row's frame (thread s runs check node
+// s - off, so edge k's column entry is s + fr_cof); frame of LDS row i for half H's phase B
+template <int BG>
+constexpr int fr_sft(int i, int k) { return zc_shift<BG, kFrZ>(BGT<BG>::RS[i] + k); }
+template <int BG>
+constexpr int fr_cof(int i, int k) { return (fr_sft<BG>(i, k) - kFrPlan<BG>.off[i] + kFrZ) % kFrZ; }
+template <int BG>
+constexpr int fr_pf(int i, int H) { return kFrPlan<BG>.kc[H][i] >= 0 ? fr_sft<BG>(i, kFrPlan<BG>.kc[H][i]) : 0; }
+// LDS rows of group g before row i
+template <int BG>
+constexpr int fr_lpos(int g, int i) {
+    int c = 0;
+    for (int x = kFrPlan<BG>.gstart[g]; x < i; ++x) c += kFrPlan<BG>.lds[x];
+    return c;
+}
+// column-(>= 2) core edges of row i before edge k
+template <int BG>
+constexpr int fr_c2(int i, int k) {
+    int c = 0;
+    for (int e = BGT<BG>::RS[i]; e < BGT<BG>::RS[i] + k; ++e) c += BGT<BG>::COL[e] >= 2 && BGT<BG>::COL[e] < BGT<BG>::KC;
+    return c;
+}
+
+// does half H add edge k of row i (a column >= 2) in phase B: LDS rows alternate edges between the
+// halves, a VGPR row's owner adds all of them
+template <int BG>
+constexpr bool fr_item(int H, int i, int k) {
+    const int j = BGT<BG>::COL[BGT<BG>::RS[i] + k];
+    if (j < 2 || j >= BGT<BG>::KC) return false;
+    return kFrPlan<BG>.lds[i] ? kFrPlan<BG>.eh[i][k] == H : kFrPlan<BG>.owner[i] == H;
+}
+// index of that add among half H's adds of group g (rows ascending, edges ascending)
+template <int BG>
+constexpr int fr_midx(int g, int H, int i, int k) {
+    int n = 0;
+    for (int r = kFrPlan<BG>.gstart[g]; r <= i && r < BGT<BG>::MB; ++r)
+        for (int kk = 0; kk < (r < i ? kFrPlan<BG>.deg(r) : k); ++kk) n += fr_item<BG>(H, r, kk);
+    return n;
+}
+template <int BG>
+constexpr int fr_maxmsg() {
+    int m = 1;
+    for (int g = 0; g < kFrPlan<BG>.ng; ++g)
+        for (int H = 0; H < 2; ++H) {
+            const int n = fr_midx<BG>(g, H, kFrPlan<BG>.gstart[g + 1], 0);
+            m = m > n ? m : n;
+        }
+    return m;
+}
+// hand-offs are read in the section before their group when pipelined: not before section 1
+template <int BG>
+constexpr bool fr_pipe_ok() {
+    for (int i = 0; i < BGT<BG>::MB; ++i)
+        if (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.grp[i] < 2) return false;
+    return true;
+}
+
+// ((e mod Zc) * 8) for 0 <= c < Zc: byte offset of entry (s + c) mod Zc from the thread's own s*8
+// and s*8 - Zc*8 (the smaller as unsigned is the valid one)
+__device__ __forceinline__ uint32_t fr_rot(uint32_t sb, uint32_t sbw, int c) {
+    if (c == 0) return sb;
+    return min(sb + (uint32_t)c * 8u, sbw + (uint32_t)c * 8u);
+}
+
+template <int BG, bool OFS>
+__global__ __launch_bounds__(kFrThreads) __attribute__((amdgpu_waves_per_eu(3))) void ldpc_frame_kernel(
+    const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
+    int32_t* __restrict__ iters, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+    const DecWork* __restrict__ work, const CbRef* __restrict__ cbs) {
+    using T = double;
+    using P = BGT<BG>;
+    constexpr int Z = kFrZ, MB = P::MB, KB = P::KB, KC = P::KC;
+    constexpr int KH = KC / 2;   // own columns: half h has column h and KH - 1 of columns >= 2
+    static_assert(KC % 2 == 0, "column split");
+    constexpr int NS = kFrPlan<BG>.nslot > 0 ? kFrPlan<BG>.nslot : 1;
+    constexpr int NPW = kFrPlan<BG>.npw > 0 ? kFrPlan<BG>.npw : 1;
+    constexpr int NLG = kFrPlan<BG>.nlg;
+    extern __shared__ __align__(16) unsigned char smem[];
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)smem != 0u)
+        __builtin_trap();   // the byte-offset LDS addressing below assumes a zero base
+    using lds_T = __attribute__((address_space(3))) T;
+    using lds_V2 = __attribute__((address_space(3))) V2<T>;
+    using lds_u32 = __attribute__((address_space(3))) uint32_t;
+    auto at = [&](uint32_t byte) -> lds_T& { return *(lds_T*)(uintptr_t)byte; };
+
+    const int t = threadIdx.x;
+    const int h = __builtin_amdgcn_readfirstlane(t / Z);
+    const int s = t - h * Z;   // own entry of every column; check node (s - off[i]) of row i
+    const T* lrow;
+    int8_t* crow;
+    int out;
+    if (work) {
+        const CbRef r = cbs[work[blockIdx.x].first];
+        lrow = llr + r.llr_off, crow = ck + r.ck_off, out = r.out;
+    } else {
+        out = (int)blockIdx.x;
+        lrow = llr + (int64_t)out * ldl, crow = ck + (int64_t)out * ldc;
+    }
+    const T* lrow_x = lrow + (KB - pc) * Z;   // extension column of row i (>= 4): lrow_x[i * Zc + z]
+    // own column jj of half h: column h, then columns 2..KH (half 0) / KH+1..KC-1 (half 1)
+    auto jcol = [&](int jj) -> int { return jj == 0 ? h : jj + 1 + h * (KH - 1); };
+    int* flagA = (int*)(smem + kFrPlan<BG>.fl_b);
+    int* anyf = flagA + 1;
+    int epoch = 0;
+    auto block_any = [&](bool p) -> bool {
+        ++epoch;
+        if (p) *anyf = epoch;
+        lds_barrier();
+        return *anyf == epoch;
+    };
+    auto per_half = [&](auto&& f) {
+        sfor<0, 2>([&](auto hc) {
+            if (h == decltype(hc)::value) f(hc);
+        });
+    };
+
+    // row state: (mA, mB), the signs of r_k (edge 0 in bit d-1) and the argmin edge
+    T sA[NS], sB[NS];
+    uint32_t sP[NPW];
+#pragma unroll
+    for (int x = 0; x < NS; ++x) sA[x] = T(0), sB[x] = T(0);
+#pragma unroll
+    for (int x = 0; x < NPW; ++x) sP[x] = 0u;
+    // LDS rows: entry (state index) e of LDS row i
+    auto lds_get = [&](auto ic, uint32_t e8, T& a, T& b, uint32_t& u, uint32_t& idx) {
+        constexpr int i = decltype(ic)::value, d = kFrPlan<BG>.deg(i);
+        // LDS rows interleaved per entry ([entry][row]): one base per entry, the row as an immediate
+        constexpr int NL = kFrPlan<BG>.nls;
+        const V2<T> v = LDPC5G_FR_ILV ? *(lds_V2*)(uintptr_t)(uint32_t)(kFrPlan<BG>.st_b + kFrPlan<BG>.lslot[i] * 16 + e8 * (2 * NL))
+                                      : *(lds_V2*)(uintptr_t)(uint32_t)(kFrPlan<BG>.st_b + kFrPlan<BG>.lslot[i] * Z * 16 + 2 * e8);
+        a = v.x, b = v.y;
+        const uint32_t p = LDPC5G_FR_ILV ? *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.pk_b + kFrPlan<BG>.lslot[i] * 4 + (e8 >> 1) * NL)
+                                         : *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.pk_b + kFrPlan<BG>.lslot[i] * Z * 4 + (e8 >> 1));
+        u = p << (32 - d), idx = p >> 24;
+        asm volatile("" : "+v"(idx));   // compare idx itself with inline constants k
+    };
+    auto get_state = [&](auto ic, T& a, T& b, uint32_t& u, uint32_t& idx) {
+        constexpr int i = decltype(ic)::value, d = kFrPlan<BG>.deg(i);
+        if constexpr (kFrPlan<BG>.lds[i]) {
+            lds_get(ic, (uint32_t)s * 8u, a, b, u, idx);
+        } else {
+            constexpr int x = kFrPlan<BG>.slot[i], w = kFrPlan<BG>.pw[i], f = kFrPlan<BG>.ph[i];
+            a = sA[x], b = sB[x];
+            const uint32_t p = sP[w];
+            if constexpr (f == 0) u = p << (32 - d), idx = p >> 24;
+            else if constexpr (f == 1) u = p << (32 - d), idx = (p >> 12) & 0xfu;
+            else u = p << (16 - d), idx = p >> 28;
+            asm volatile("" : "+v"(idx));
+        }
+    };
+    auto put_state = [&](auto ic, T a, T b, uint32_t negs, uint32_t idx) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (kFrPlan<BG>.lds[i]) {
+            V2<T> v;
+            v.x = a, v.y = b;
+            constexpr int NL = kFrPlan<BG>.nls;
+            const uint32_t e8 = (uint32_t)s * 8u;
+            *(lds_V2*)(uintptr_t)(uint32_t)(LDPC5G_FR_ILV ? kFrPlan<BG>.st_b + kFrPlan<BG>.lslot[i] * 16 + e8 * (2 * NL)
+                                                          : kFrPlan<BG>.st_b + kFrPlan<BG>.lslot[i] * Z * 16 + 2 * e8) = v;
+            *(lds_u32*)(uintptr_t)(uint32_t)(LDPC5G_FR_ILV ? kFrPlan<BG>.pk_b + kFrPlan<BG>.lslot[i] * 4 + (e8 >> 1) * NL
+                                                           : kFrPlan<BG>.pk_b + kFrPlan<BG>.lslot[i] * Z * 4 + (e8 >> 1)) = negs | (idx << 24);
+        } else {
+            constexpr int x = kFrPlan<BG>.slot[i], w = kFrPlan<BG>.pw[i], f = kFrPlan<BG>.ph[i];
+            sA[x] = a, sB[x] = b;
+            if constexpr (f == 0) sP[w] = negs | (idx << 24);
+            else if constexpr (f == 1) sP[w] = (sP[w] & 0xffff0000u) | negs | (idx << 12);
+            else sP[w] = (sP[w] & 0xffffu) | (negs << 16) | (idx << 28);
+        }
+    };
+
+    // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS state 0; wrap table; flags
+    {
+        T v0[KH];
+#pragma unroll
+        for (int jj = 0; jj < KH; ++jj) {
+            const int j = jcol(jj);
+            v0[jj] = lrow[(j < pc ? 0 : j - pc) * Z + s];
+        }
+#pragma unroll
+        for (int jj = 0; jj < KH; ++jj) {
+            const int j = jcol(jj);
+            at((uint32_t)(j * kFrColB + s * 8)) = j < pc ? T(0) : v0[jj];
+        }
+    }
+    for (int w = t; w < kFrPlan<BG>.nls * Z; w += kFrThreads) {
+        V2<T> v;
+        v.x = T(0), v.y = T(0);
+        *(lds_V2*)(uintptr_t)(uint32_t)(kFrPlan<BG>.st_b + w * 16) = v;
+        *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.pk_b + w * 4) = 0u;
+    }
+    // wrap table: entry e < 2*Zc holds (e mod Zc) * 8
+    *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.tbl_b + t * 4) = (uint32_t)s * 8u;
+    if (t == 0) *flagA = 0, *anyf = 0;
+    lds_barrier();
+
+    const uint32_t sb0 = (uint32_t)s * 8u, sbw0 = sb0 - (uint32_t)(Z * 8);
+    const uint32_t tz0 = (uint32_t)(kFrPlan<BG>.tbl_b + s * 4);
+    uint32_t mv = 0x80000000u;   // sign mask kept in a VGPR (all-VGPR bitop3 is full rate)
+    asm volatile("" : "+v"(mv));
+    bool active = true;
+    uint64_t hdx_keep = 0;   // extension decisions of a codeblock decided by the syndrome test
+    int it = 0;
+    for (; it < L; ++it) {
+        // opaque per iteration: otherwise LICM hoists hundreds of loop-invariant addresses
+        uint32_t sb = sb0, sbw = sbw0, tz = tz0;
+        int sv = s;
+        asm volatile("" : "+v"(sb));
+        asm volatile("" : "+v"(sbw));
+        asm volatile("" : "+v"(tz));
+        asm volatile("" : "+v"(sv));
+        auto rot = [&](int c) -> uint32_t { return fr_rot(sb, sbw, c); };
+        // check node of row i run by this thread: (s - off[i]) mod Zc
+        auto xpos = [&](int i) -> int {
+            const int c = (Z - kFrPlan<BG>.off[i]) % Z;
+            if (c == 0) return sv;
+            return (int)min((uint32_t)(sv + c), (uint32_t)(sv + c - Z));
+        };
+        auto llrx = [&](int i) -> T { return lrow_x[i * Z + xpos(i)]; };
+        bool fail = false;
+        uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
+
+        // ext LLR ring: slot p % XP holds the LLR of the half's ext row p, loaded XP rows ahead
+        constexpr int XP = kXPre > 0 ? kXPre : 1;
+        T xr[XP];
+        auto xload = [&](auto hc, auto pc_) {
+            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
+            if constexpr (p < kFrPlan<BG>.nx[hh]) xr[p % XP] = llrx(kFrPlan<BG>.xlist[hh][p]);
+        };
+        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202); core-edge
+        // LQ reads one edge ahead, their wrap-table offsets two ahead
+        struct RowSt {
+            T mA, mB, min1, min2;
+            uint32_t u, idxo, idx, negs;
+            bool par;
+            T ab;
+            uint32_t tb[2];
+        };
+        auto aloadt = [&](RowSt& r, auto ic, auto kc3) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k3 = decltype(kc3)::value;
+            if constexpr (k3 < d)
+                if constexpr (P::COL[e0 + k3] < KC) r.tb[k3 % 2] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k3) * 4u);
+        };
+        auto aload = [&](RowSt& r, auto ic, auto kc2) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k2 = decltype(kc2)::value;
+            if constexpr (k2 < d)
+                if constexpr (P::COL[e0 + k2] < KC) r.ab = at((uint32_t)(P::COL[e0 + k2] * kFrColB) + r.tb[k2 % 2]);
+        };
+        auto rowA = [&](auto ic) {
+            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
+            RowSt r;
+            get_state(ic, r.mA, r.mB, r.u, r.idxo);
+            r.min1 = FT<T>::inf(), r.min2 = FT<T>::inf();
+            r.idx = 0, r.negs = 0, r.par = false;
+            aloadt(r, ic, std::integral_constant<int, 0>{});
+            aloadt(r, ic, std::integral_constant<int, 1>{});
+            aload(r, ic, std::integral_constant<int, 0>{});
+            sfor<0, d>([&](auto kc) {
+                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
+                const T rold = xsign_v(pick(r.idxo == (uint32_t)k, r.mB, r.mA), r.u, mv);
+                asm("v_add_u32 %0, %1, %1" : "=v"(r.u) : "v"(r.u));   // u <<= 1, all-VGPR form
+                T a;
+                if constexpr (j < KC) {
+                    a = r.ab;
+                    aload(r, ic, std::integral_constant<int, k + 1>{});
+                    aloadt(r, ic, std::integral_constant<int, k + 2>{});
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+                    constexpr int hh = kFrPlan<BG>.owner[i], p = kFrPlan<BG>.xpos[i];
+                    a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
+                    xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
+                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
+                }
+                r.par ^= a < T(0);
+                const T q = a - rold;
+                const T aq = fabs(q);
+                r.idx = aq < r.min1 ? (uint32_t)k : r.idx;
+                asm volatile("" : "+v"(r.idx));
+                r.negs = __builtin_amdgcn_alignbit(r.negs, FT<T>::sbits(q), 31);
+                two_min(r.min1, r.min2, aq);
+            });
+            fail |= r.par;
+            T x1 = r.min1, x2 = r.min2;
+            if constexpr (OFS) {
+                x1 = r.min1 - beta, x2 = r.min2 - beta;   // max(minv - beta, 0) (:201)
+                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
+            }
+            const uint32_t sgn = 0u - (__builtin_popcount(r.negs) & 1u);   // the row's sign product
+            put_state(ic, alpha * x1, alpha * x2, r.negs ^ (sgn & ((1u << d) - 1u)), r.idx);
+        };
+        if (active) {
+            per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
+            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
+                if (h == kFrPlan<BG>.owner[decltype(ic)::value]) rowA(ic);
+            });
+            if (fail) *flagA = 1;
+        }
+        lds_barrier();
+        // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
+        if (active && *flagA == 0) {
+            hdx_keep = hdx;   // the LQ image stays frozen (no phase B) for the decisions
+            if (t == 0) status[out] = 1, iters[out] = it;
+            active = false;
+        }
+
+        // ---- phase B: Lr.sum(axis=0) in row order (:126).  Columns >= 2: ds_add into the LQ
+        // image, one barrier per group; column h: this thread's register sum S.
+        auto msg = [&](T a, T b, uint32_t u, uint32_t idx, auto kc) -> T {
+            constexpr int k = decltype(kc)::value;
+            return xsign_v(pick(idx == (uint32_t)k, b, a), u << k, mv);
+        };
+        auto add_to = [&](auto ic, auto kc, T r, uint32_t ent) {   // column of edge k of row i
+            constexpr int i = decltype(ic)::value, k = decltype(kc)::value, j = P::COL[P::RS[i] + k];
+            lds_T& acc = at((uint32_t)(j * kFrColB) + ent);
+            if constexpr (kFrPlan<BG>.first_row[j] == i) acc = T(0) + r;
+            else __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        T S = T(0);
+        // phase-B entry offset: arithmetic or the wrap table
+        auto brot = [&](int c) -> uint32_t {
+            if constexpr (LDPC5G_FR_BTAB) return *(lds_u32*)(uintptr_t)(tz + (uint32_t)c * 4u);
+            else return rot(c);
+        };
+        // the core LLRs of the LQ update, loaded early so phase B hides their latency
+        T lf[KH];
+        auto lf_load = [&]() {
+#pragma unroll
+            for (int jj = 0; jj < KH; ++jj) {
+                const int j = jcol(jj);
+                lf[jj] = lrow[(j < pc ? 0 : j - pc) * Z + sv];
+            }
+        };
+        constexpr int kLfG = [] {
+            if (LDPC5G_FR_LFG < 0) return -1;
+            int g = 0;
+            for (int i = 0; i < MB; ++i)
+                if (kFrPlan<BG>.lds[i]) g = kFrPlan<BG>.grp[i] + 1 + LDPC5G_FR_LFG;
+            return g < kFrPlan<BG>.ng ? g : kFrPlan<BG>.ng - 1;
+        }();
+        if (active) {
+            if constexpr (kLfG < 0) lf_load();
+            // hand-offs: the other column's message of this half's rows with both columns
+            per_half([&](auto hc) {
+                constexpr int H = decltype(hc)::value;
+                sfor<0, MB>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.owner[i] == H) {
+                        constexpr int k = kFrPlan<BG>.kc[1 - H][i];
+                        T a, b;
+                        uint32_t u, idx;
+                        get_state(ic, a, b, u, idx);
+                        at((uint32_t)kFrPlan<BG>.hb(kFrPlan<BG>.ho[i]) + brot(fr_cof<BG>(i, k))) = msg(a, b, u, idx, std::integral_constant<int, k>{});
+                    }
+                });
+            });
+        }
+        // LDS rows' state of a group, read in this half's frame (LDPC5G_FR_PREF: one group ahead)
+        T qa[NLG] = {}, qb[NLG] = {};
+        uint32_t qu[NLG] = {}, qi[NLG] = {};
+        auto prefetch = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            per_half([&](auto hc) {
+                constexpr int H = decltype(hc)::value;
+                sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if constexpr (kFrPlan<BG>.lds[i]) {
+                        constexpr int n = fr_lpos<BG>(g, i);
+                        lds_get(ic, rot((Z - fr_pf<BG>(i, H)) % Z), qa[n], qb[n], qu[n], qi[n]);
+                    }
+                });
+            });
+        };
+        if constexpr (LDPC5G_FR_PIPE) {
+            static_assert(fr_pipe_ok<BG>(), "hand-off read before its write's barrier");
+            constexpr int MM = fr_maxmsg<BG>();
+            T pm[MM];
+            uint32_t pad[LDPC5G_FR_PIPEA ? MM : 1];
+            // chain steps and the messages (value, LDS byte address) of this half's adds of group g
+            auto prepare = [&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                per_half([&](auto hc) {
+                    constexpr int H = decltype(hc)::value;
+                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
+                        constexpr bool mine = kFrPlan<BG>.lds[i] || kFrPlan<BG>.owner[i] == H;
+                        if constexpr (mine) {
+                            // the state at check node (s - Pf) mod Zc: this half's frame
+                            constexpr int Pf = kFrPlan<BG>.lds[i] ? fr_pf<BG>(i, H) : kFrPlan<BG>.off[i];
+                            T a, b;
+                            uint32_t u, idx;
+                            if constexpr (kFrPlan<BG>.lds[i]) lds_get(ic, rot((Z - Pf) % Z), a, b, u, idx);
+                            else get_state(ic, a, b, u, idx);
+                            sfor<0, d>([&](auto kc) {
+                                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
+                                if constexpr (j == H) {
+                                    S = S + xsign_v(pick(idx == (uint32_t)k, b, a), u, mv);
+                                } else if constexpr (fr_item<BG>(H, i, k)) {
+                                    constexpr int n = fr_midx<BG>(g, H, i, k);
+                                    pm[n] = xsign_v(pick(idx == (uint32_t)k, b, a), u, mv);
+                                    if constexpr (LDPC5G_FR_PIPEA)
+                                        pad[n] = (uint32_t)(j * kFrColB) + brot((fr_sft<BG>(i, k) - Pf + Z) % Z);
+                                }
+                                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
+                            });
+                        } else if constexpr (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.kc[H][i] >= 0) {
+                            S = S + at((uint32_t)kFrPlan<BG>.hb(kFrPlan<BG>.ho[i]) + sb);   // the owner's hand-off
+                        }
+                    });
+                });
+            };
+            auto issue = [&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                per_half([&](auto hc) {
+                    constexpr int H = decltype(hc)::value;
+                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        sfor<0, kFrPlan<BG>.deg(i)>([&](auto kc) {
+                            constexpr int k = decltype(kc)::value, j = P::COL[P::RS[i] + k];
+                            if constexpr (fr_item<BG>(H, i, k)) {
+                                constexpr int n = fr_midx<BG>(g, H, i, k);
+                                constexpr int Pf = kFrPlan<BG>.lds[i] ? fr_pf<BG>(i, H) : kFrPlan<BG>.off[i];
+                                lds_T& acc = LDPC5G_FR_PIPEA ? *(lds_T*)(uintptr_t)pad[n]
+                                                             : at((uint32_t)(j * kFrColB) + rot((fr_sft<BG>(i, k) - Pf + Z) % Z));
+                                if constexpr (kFrPlan<BG>.first_row[j] == i) acc = T(0) + pm[n];
+                                else __hip_atomic_fetch_add(&acc, pm[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        });
+                    });
+                });
+            };
+            if (active) prepare(std::integral_constant<int, 0>{});
+            sfor<0, kFrPlan<BG>.ng>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                if (active) {
+                    issue(gc);
+                    if constexpr (g == kLfG) lf_load();
+                    if constexpr (g + 1 < kFrPlan<BG>.ng) prepare(std::integral_constant<int, g + 1>{});
+                }
+                lds_barrier();
+            });
+        } else {
+        if (LDPC5G_FR_PREF && active) prefetch(std::integral_constant<int, 0>{});
+        sfor<0, kFrPlan<BG>.ng>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            T ca[NLG], cb[NLG];
+            uint32_t cu[NLG], ci[NLG];
+            if (active) {
+                if constexpr (!LDPC5G_FR_PREF) prefetch(gc);
+#pragma unroll
+                for (int n = 0; n < NLG; ++n) ca[n] = qa[n], cb[n] = qb[n], cu[n] = qu[n], ci[n] = qi[n];
+                if constexpr (LDPC5G_FR_PREF && g + 1 < kFrPlan<BG>.ng) prefetch(std::integral_constant<int, g + 1>{});
+                if constexpr (g == kLfG) lf_load();
+                per_half([&](auto hc) {
+                    constexpr int H = decltype(hc)::value;
+                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
+                        if constexpr (kFrPlan<BG>.lds[i]) {
+                            // both halves: column H's message and alternate edges of columns >= 2,
+                            // from the state at check node (s - P) mod Zc, P = V(i, H) (or 0)
+                            constexpr int n = fr_lpos<BG>(g, i);
+                            constexpr int Pf = fr_pf<BG>(i, H);
+                            const T a = ca[n], b = cb[n];
+                            const uint32_t u = cu[n], idx = ci[n];
+                            uint32_t uw = u;   // !LDPC5G_FR_USH: sign word walked edge by edge
+                            sfor<0, d>([&](auto kc) {
+                                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
+                                if constexpr (j == H) {
+                                    S = S + xsign_v(pick(idx == (uint32_t)k, b, a), LDPC5G_FR_USH ? u << k : uw, mv);
+                                } else if constexpr (fr_item<BG>(H, i, k)) {
+                                    add_to(ic, kc, xsign_v(pick(idx == (uint32_t)k, b, a), LDPC5G_FR_USH ? u << k : uw, mv),
+                                           brot((fr_sft<BG>(i, k) - Pf + Z) % Z));
+                                }
+                                if constexpr (!LDPC5G_FR_USH) asm("v_add_u32 %0, %1, %1" : "=v"(uw) : "v"(uw));
+                            });
+                        } else if constexpr (kFrPlan<BG>.owner[i] == H) {
+                            T a, b;
+                            uint32_t u, idx;
+                            get_state(ic, a, b, u, idx);
+                            uint32_t uw = u;
+                            sfor<0, d>([&](auto kc) {
+                                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
+                                if constexpr (j == H) {
+                                    S = S + xsign_v(pick(idx == (uint32_t)k, b, a), LDPC5G_FR_USH ? u << k : uw, mv);
+                                } else if constexpr (j >= 2 && j < KC) {
+                                    add_to(ic, kc, xsign_v(pick(idx == (uint32_t)k, b, a), LDPC5G_FR_USH ? u << k : uw, mv), brot(fr_cof<BG>(i, k)));
+                                }
+                                if constexpr (!LDPC5G_FR_USH) asm("v_add_u32 %0, %1, %1" : "=v"(uw) : "v"(uw));
+                            });
+                        } else if constexpr (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.kc[H][i] >= 0) {
+                            S = S + at((uint32_t)kFrPlan<BG>.hb(kFrPlan<BG>.ho[i]) + sb);   // the owner's hand-off
+                        }
+                    });
+                });
+            }
+            lds_barrier();
+        });
+        }
+        // ---- LQ = LLRin + sum (:126) for the own entries
+        if (active) {
+#pragma unroll
+            for (int jj = 0; jj < KH; ++jj) {
+                const int j = jcol(jj);
+                lds_T& x = at((uint32_t)(j * kFrColB) + sb);
+                x = (j < pc ? T(0) : lf[jj]) + (jj == 0 ? S : x);   // punctured columns: LLR 0 (:43)
+            }
+        }
+        if (t == 0) *flagA = 0;   // read before the phase-B barriers
+        if (!block_any(active)) break;
+    }
+
+    // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
+    int sv = s;
+    asm volatile("" : "+v"(sv));   // keep the output addresses out of the loop
+    uint32_t sb = sb0, sbw = sbw0;
+    asm volatile("" : "+v"(sb));
+    asm volatile("" : "+v"(sbw));
+    auto xposf = [&](int i) -> int {
+        const int c = (Z - kFrPlan<BG>.off[i]) % Z;
+        if (c == 0) return sv;
+        return (int)min((uint32_t)(sv + c), (uint32_t)(sv + c - Z));
+    };
+    uint32_t oc = 0;          // own core columns (bit jj): LQ <= 0, or LQ_old < 0 if decided
+    uint64_t ox = hdx_keep;   // own extension columns (check node of the row's frame)
+    if (active) {
+        ox = 0;
+        per_half([&](auto hc) {
+            constexpr int hh = decltype(hc)::value, NX = kFrPlan<BG>.nx[hh], XB = 8;
+            sfor<0, (NX + XB - 1) / XB>([&](auto bc) {
+                constexpr int x0 = decltype(bc)::value * XB, x1 = x0 + XB < NX ? x0 + XB : NX;
+                T vx[XB];
+                sfor<x0, x1>([&](auto xc) {
+                    constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
+                    vx[decltype(xc)::value - x0] = lrow_x[i * Z + xposf(i)];
+                });
+                __builtin_amdgcn_sched_barrier(0);
+                sfor<x0, x1>([&](auto xc) {
+                    constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
+                    constexpr int dl = kFrPlan<BG>.deg(i) - 1;   // ext column = last edge
+                    T a, b;
+                    uint32_t u, idx;
+                    get_state(std::integral_constant<int, i>{}, a, b, u, idx);
+                    const T r = xsign_v(pick(idx == (uint32_t)dl, b, a), u << dl, mv);
+                    ox |= (uint64_t)(vx[decltype(xc)::value - x0] + r <= T(0)) << (i - 4);
+                });
+            });
+        });
+        bool fail = false;
+        per_half([&](auto hc) {
+            constexpr int hh = decltype(hc)::value;
+            constexpr uint64_t rows = [] {
+                uint64_t m = 0;
+                for (int i = 0; i < P::MB; ++i)
+                    if (kFrPlan<BG>.owner[i] == hh) m |= 1ull << i;
+                return m;
+            }();
+            fail = syndrome_fails<BG, rows, false, T>(
+                [&](auto ic, auto kc) -> T {
+                    constexpr int i = decltype(ic)::value, k = decltype(kc)::value;
+                    constexpr int c = (fr_sft<BG>(i, k) - kFrPlan<BG>.off[i] + Z) % Z;
+                    return at((uint32_t)(P::COL[P::RS[i] + k] * kFrColB) + fr_rot(sb, sbw, c));
+                },
+                [&](auto ic) -> bool { return (ox >> (decltype(ic)::value - 4)) & 1u; });
+        });
+        if (fail) *flagA = 1;
+    }
+#pragma unroll
+    for (int jj = 0; jj < KH; ++jj) {
+        const T v = at((uint32_t)(jcol(jj) * kFrColB) + sb);
+        oc |= (uint32_t)(active ? v <= T(0) : v < T(0)) << jj;
+    }
+    lds_barrier();   // every LQ / state read is done: LDS below the flags is free from here
+    if (active && t == 0) {
+        status[out] = *flagA == 0;
+        iters[out] = L;
+    }
+    // ---- ck through LDS (ck_store_staged, ldpc5g_dec_body.h)
+    constexpr int NFZ = P::NB * Z;
+    static_assert(NFZ <= kFrPlan<BG>.fl_b, "ck staging below the flags");
+#pragma unroll
+    for (int jj = 0; jj < KH; ++jj) ck_stage_byte((uint32_t)(jcol(jj) * Z + sv), (oc >> jj) & 1u);
+    per_half([&](auto hc) {
+        sfor<4, MB>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (kFrPlan<BG>.owner[i] == decltype(hc)::value)
+                ck_stage_byte((uint32_t)((KB + i) * Z + xposf(i)), (uint32_t)(ox >> (i - 4)) & 1u);
+        });
+    });
+    const bool slow = block_any(!ck_row_aligned(NFZ, crow));   // orders the staging too
+    ck_store_staged(NFZ, 1, [&](int) -> int8_t* { return crow; }, slow, t, kFrThreads);
+}
+
+template <int BG>
+int launch_frame_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg, int64_t ldl,
+                   int64_t ldc, int L, double alpha, double beta, int pc, const DecWork* work,
+                   const CbRef* cbs, hipStream_t st) {
+    const bool ofs = beta != 0.0;
+    constexpr size_t lds = (size_t)kFrPlan<BG>.bytes;
+    if (int rc = ofs ? set_lds_once<ldpc_frame_kernel<BG, true>>(lds) : set_lds_once<ldpc_frame_kernel<BG, false>>(lds))
+        return rc;
+    auto kern = ofs ? ldpc_frame_kernel<BG, true> : ldpc_frame_kernel<BG, false>;
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(kFrThreads), lds, st, llr, ck, status, iters, ldl, ldc, L, alpha,
+                       beta, pc, work, cbs);
+    return check_hip(hipGetLastError(), "ldpc_frame_kernel launch");
+}
+
+}  // namespace
+}  // namespace ldpc5g_impl

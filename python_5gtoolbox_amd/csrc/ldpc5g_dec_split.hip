@@ -39,6 +39,13 @@ namespace {
 constexpr int kSplitThreads = 1024;
 constexpr int kSplitSync = 64;   // sync words per codeblock (a 256-B line): barrier counter, flags
 constexpr int kSplitMaxWG = 224;   // of the 256 CUs, one workgroup each (7/8 of a device's CUs)
+// A barrier wait gives up after this many ticks of the 100 MHz real-time clock (4 s; a barrier takes
+// microseconds).  The parts of a codeblock must be resident together; if some never get a CU (other
+// kernels holding the device), the waiting parts abort instead of hanging the GPU: bit 31 of the
+// codeblock's barrier counter (sticky: every part's poll ends on it), status 0, iters -1, the
+// device's timeout count + 1 (ldpc5g_split_timeouts), and the last part out clears the sync words.
+constexpr uint64_t kSplitTimeoutTicks = 400000000ull;
+constexpr uint32_t kSplitAbort = 0x80000000u;
 // loads in flight per chunk (phase A LQ reads, phase B message reads); 32: a row's / column's all
 // at once (r05, one BG1 Zc=384 codeblock: 10 / 10 100 us per call, all 87 us)
 #ifndef LDPC5G_SPLIT_CH
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     // loads in flight per chunk (phase A, B); R = 2 keeps twice the chunk state, so fewer
     constexpr int CH = R == 1 ? LDPC5G_SPLIT_CH : 16, CCH = R == 1 ? LDPC5G_SPLIT_CCH : 16;
     __shared__ uint32_t rws[MB * DMAX], wws[MB * DMAX];   // edge words per (row, edge < DMAX)
-    __shared__ uint32_t lfail, lflag, lticket;
+    __shared__ uint32_t lfail, lflag, lticket, labort;
 
     const int t = threadIdx.x, lane = t & 63;
     const int v = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
         // the last ticket of the launch: every workgroup holds its own, the counter goes back to 0
         if (tk == gridDim.x - 1u)
             __hip_atomic_store((g_u32*)(uintptr_t)ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lticket = tk, lfail = 0u;
+        lticket = tk, lfail = 0u, labort = 0u;
     }
     __syncthreads();
     const int tkt = __builtin_amdgcn_readfirstlane((int)lticket);
@@ -176,11 +183,13 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     double* lq = scratch + (size_t)cb * split_rows<BG>() * Zc;   // [KC][Zc] LQ of the core columns
     double* msg = lq + (size_t)KC * Zc;                            // [NCE][Zc] messages, CSC slots
     uint32_t* sy = sync + cb * kSplitSync;   // [0] barrier counter, [1] fail tag, [2] final fail, [3] exits
+    uint32_t* timeouts = ticket + 1;         // the device's count of timed-out codeblocks
 
     // barrier over the codeblock's W workgroups.  sig: this workgroup's fail tag (LDS lfail) is
     // raised into sy[fi] first; afterwards lflag = sy[fi] for every thread of the workgroup.
+    // Returns false when the codeblock was aborted (kSplitTimeoutTicks): the caller returns.
     uint32_t nbar = 0;
-    auto grid_sync = [&](int fi, uint32_t sig) {
+    auto grid_sync = [&](int fi, uint32_t sig) -> bool {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's hand-off stores done
         __syncthreads();
         nbar += (uint32_t)W;
@@ -190,10 +199,30 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __hip_atomic_fetch_add((g_u32*)(uintptr_t)sy, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (ld_sc1(sy) < nbar) __builtin_amdgcn_s_sleep(1);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t c;
+            while ((c = ld_sc1(sy)) < nbar) {   // an aborted counter (bit 31) ends the wait too
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kSplitTimeoutTicks) {
+                    __hip_atomic_fetch_or((g_u32*)(uintptr_t)sy, kSplitAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    c = kSplitAbort;
+                    break;
+                }
+            }
+            labort = c & kSplitAbort;
             lflag = ld_sc1(sy + fi);
         }
         __syncthreads();
+        if (labort == 0u) return true;
+        if (t == 0) {   // every part ends up here once: the last one out counts and cleans up
+            status[cb] = 0, iters[cb] = -1;
+            if (__hip_atomic_fetch_add((g_u32*)(uintptr_t)(sy + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (uint32_t)(W - 1)) {
+                __hip_atomic_fetch_add((g_u32*)(uintptr_t)timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sync_clear(sy);
+            }
+        }
+        return false;
     };
 
     const int nch = (Zc + 63) >> 6;   // chunks per row / column
@@ -232,7 +261,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
     asm volatile("" : "+v"(mv));
     // iteration 0's phase A reads LQ_0 = the LLRs straight from the input (punctured columns 0), so
     // no barrier is needed before it; only L = 0 reads the scratch LQ (the final pass) right away
-    if (L == 0) grid_sync(1, 0u);
+    if (L == 0 && !grid_sync(1, 0u)) return;
     SPLIT_TS(1);
     const uint32_t pcZT = (uint32_t)pc * ZT;
     const char* lrowb = (const char*)lrow - pcZT;   // byte offset col*ZT + z*8 of LQ_0 (col >= pc)
@@ -331,7 +360,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
             phase_a(std::false_type{});
         if (fail) lfail = (uint32_t)(it + 1);
         if (it < 2) SPLIT_TS(2 + 4 * it);
-        grid_sync(1, (uint32_t)(it + 1));
+        if (!grid_sync(1, (uint32_t)(it + 1))) return;
         if (it < 2) SPLIT_TS(3 + 4 * it);
         if (lflag != (uint32_t)(it + 1)) {
             // ---- the syndrome of LQ_old holds (:112-114): its hard decisions are the output
@@ -375,7 +404,7 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
             }
         });
         if (it < 2) SPLIT_TS(4 + 4 * it);
-        grid_sync(1, 0u);
+        if (!grid_sync(1, 0u)) return;
         if (it < 2) SPLIT_TS(5 + 4 * it);
     }
 
@@ -431,6 +460,20 @@ __global__ __launch_bounds__(kSplitThreads) void ldpc_split_kernel(
 #endif
 }
 
+// per-device state of the split launches (both base graphs): the chain event, the sync area
+// (kSplitMaxWG codeblock lines + the ticket line: [0] ticket, [1] timed-out codeblocks), the scratch
+struct SplitState {
+    std::mutex mu;
+    hipEvent_t last[64] = {};
+    uint32_t* sync[64] = {};
+    void* scratch[64] = {};
+    size_t cap[64] = {};
+};
+SplitState& split_state() {
+    static SplitState s;
+    return s;
+}
+
 template <int BG>
 int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B, int Zc,
                    int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
@@ -439,24 +482,22 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
     if (R == 0) return fail(LDPC5G_ESIZE, "split decoder: %d codeblocks of Zc=%d do not fit", B, Zc);
     const int W = split_parts(BG, Zc, R);
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (dev < 0 || dev >= 64) return fail(LDPC5G_ESIZE, "device ordinal %d >= 64", dev);
     const size_t bytes = (size_t)B * split_rows<BG>() * Zc * sizeof(double);
     int rc = 0;
     {
-        // split launches of one device run one after another, whatever their streams (a per-device
-        // event chain; on one stream it costs nothing), so they share one scratch and one sync area
-        // per device, plain hipMalloc memory (the hand-off table's row): the scratch grows on
-        // demand (after the previous launch has ended), the sync area is zeroed once and every
-        // launch leaves its words zero again (sync_clear), so no allocation or memset runs per call
-        static std::mutex mu;
-        static hipEvent_t last[64] = {};
-        static uint32_t* sync_area[64] = {};
-        static void* scratch_area[64] = {};
-        static size_t scratch_cap[64] = {};
-        std::lock_guard<std::mutex> lk(mu);
-        hipEvent_t& ev = last[dev & 63];
-        uint32_t*& sync = sync_area[dev & 63];
-        void*& p = scratch_area[dev & 63];
+        // split launches of one device run one after another, whatever their streams and base
+        // graphs (a per-device event chain; on one stream it costs nothing), so they share one
+        // scratch and one sync area per device, plain hipMalloc memory (the hand-off table's row):
+        // the scratch grows on demand (after the previous launch has ended), the sync area is
+        // zeroed once and every launch leaves its words zero again (sync_clear), so no allocation
+        // or memset runs per call
+        SplitState& S = split_state();
+        std::lock_guard<std::mutex> lk(S.mu);
+        hipEvent_t& ev = S.last[dev];
+        uint32_t*& sync = S.sync[dev];
+        void*& p = S.scratch[dev];
         if (!sync) {
             const size_t sb = ((size_t)kSplitMaxWG + 1) * kSplitSync * 4;   // + the ticket line
             void* q = nullptr;
@@ -465,16 +506,16 @@ int launch_split_t(const double* llr, int8_t* ck, uint8_t* status, int32_t* iter
             if (!rc) rc = check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (split sync area)");
             if (!rc) sync = (uint32_t*)q;
         }
-        if (!rc && scratch_cap[dev & 63] < bytes) {
+        if (!rc && S.cap[dev] < bytes) {
             if (p) {
                 if (ev) rc = check_hip(hipEventSynchronize(ev), "hipEventSynchronize (split scratch)");
                 if (!rc) rc = check_hip(hipFree(p), "hipFree (split scratch)");
-                p = nullptr, scratch_cap[dev & 63] = 0;
+                p = nullptr, S.cap[dev] = 0;
             }
             // at least 24 BG1 Zc = 384 codeblocks' worth (20 MB), so most devices allocate once
             const size_t want = std::max(bytes, (size_t)24 * split_rows<1>() * 384 * sizeof(double));
             if (!rc) rc = check_hip(hipMalloc(&p, want), "hipMalloc (split scratch)");
-            if (!rc) scratch_cap[dev & 63] = want;
+            if (!rc) S.cap[dev] = want;
         }
         if (rc) {
         } else if (!ev) {
@@ -512,16 +553,31 @@ int split_wanted(int bgn, int B, int Zc) {
     static std::atomic<int> cus_of[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
-    int cus = cus_of[dev & 63].load(std::memory_order_relaxed);
+    if (dev < 0 || dev >= 64) return 0;   // (the split launcher refuses such devices)
+    int cus = cus_of[dev].load(std::memory_order_relaxed);
     if (cus == 0) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
-        cus_of[dev & 63].store(cus, std::memory_order_relaxed);
+        cus_of[dev].store(cus, std::memory_order_relaxed);
     }
     const int maxwg = std::min(kSplitMaxWG, cus * 7 / 8);
     const int w1 = split_parts(bgn, Zc, 1), w2 = split_parts(bgn, Zc, 2);
     if (w1 <= cus && B * w1 <= maxwg) return 1;
     if (w2 <= cus && B * w2 <= maxwg) return 2;
     return 0;
+}
+
+int split_timeouts(uint32_t* count) {
+    int dev = 0;
+    if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (dev < 0 || dev >= 64) return fail(LDPC5G_ESIZE, "device ordinal %d >= 64", dev);
+    SplitState& S = split_state();
+    std::lock_guard<std::mutex> lk(S.mu);
+    *count = 0;
+    if (!S.sync[dev]) return LDPC5G_OK;   // no split launch on this device yet
+    if (S.last[dev])
+        if (int rc = check_hip(hipEventSynchronize(S.last[dev]), "hipEventSynchronize (split chain)")) return rc;
+    return check_hip(hipMemcpy(count, S.sync[dev] + kSplitMaxWG * kSplitSync + 1, sizeof(uint32_t),
+                               hipMemcpyDeviceToHost), "hipMemcpy (split timeouts)");
 }
 
 int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int B,

@@ -450,8 +450,13 @@ __global__ __launch_bounds__(kRrNT) void raterecover_kernel(const Tin* __restric
     // pass 1 writes every k < size — final (0.0 + x) / 1 for ranks visited once, the raw LLR for
     // ranks visited twice — and after a barrier pass 2 combines each k >= size with it as
     // (0.0 + x0 + x1) / 2, the reference's float64 sum of the two tmp_buf rows (:53-58).
-    const int E2 = E - s.size;   // ranks [0, E2) are visited twice
-    const bool kmaj = E <= s.size || (sizeof(Tout) >= sizeof(Tin) && E <= 2 * s.size);
+    // ranks [0, E2) are visited twice.  Pass 1 parks the first visit's LLR in the output row, so
+    // when the HARQ input IS the output row (in-place combining with the previous llr_dn) pass 2
+    // would read that LLR instead of the previous value: such rows take the gather below, which
+    // reads harq[p] and writes out[p] in one thread.
+    const int E2 = E - s.size;
+    const bool kmaj = E <= s.size || (sizeof(Tout) >= sizeof(Tin) && E <= 2 * s.size &&
+                                      (const void*)harq != (const void*)out);
     auto pos = [&](int rank) {   // rank in [0, size) -> position in the row
         int pp = rank + s.start;   // in the filler-free index space
         if (pp >= s.size) pp -= s.size;

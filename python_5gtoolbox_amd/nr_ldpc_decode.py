@@ -126,6 +126,10 @@ def _decode_one(LLRin, Zc, bgn, L, algo, alpha, beta, full):
         _lib.check(_lib.lib().ldpc5g_decode_ms_host(
             x.ctypes.data, ck.ctypes.data, st.ctypes.data, it.ctypes.data, 1, bgn, Zc, int(L),
             float(alpha), float(beta), flags, _lib.stream_ptr()))
+        if it[0] < 0:   # the multi-workgroup kernel gave up waiting for co-resident parts
+            raise _lib.LdpcLibError("nr_decode_ldpc: the multi-workgroup decode timed out waiting for "
+                                    "its workgroups to be co-resident (include/ldpc5g.h, "
+                                    "ldpc5g_split_timeouts); the GPU is held by other kernels")
         return ck, bool(st[0])
     dev = t.cuda.current_device()
     n_in = Nf if full else N

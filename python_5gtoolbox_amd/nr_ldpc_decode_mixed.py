@@ -47,12 +47,13 @@ def decode_mixed(items, L, alpha=1.0, beta=0.0, schedule="flooding", rate_matche
 
 class MixedBatch:
     """A device-resident mixed-(bgn, Zc) batch for repeated decoding (the bench's config 4):
-    rows of several (bgn, Zc) groups concatenated in one flat float32 LLR buffer, with the
-    descriptor array (ldpc5g_cb_desc_t) built once.
+    rows of several (bgn, Zc) groups concatenated in one flat LLR buffer, with the descriptor
+    array (ldpc5g_cb_desc_t) built once.
 
-    groups: list of (bgn, Zc, llr (n, N) float32 device tensor).  flat: an existing flat float32
-    buffer holding exactly those rows back to back in group order (e.g. sch_raterecover_multi's
-    output, whose row groups are views of it): used in place, nothing is copied."""
+    groups: list of (bgn, Zc, llr (n, N) device tensor), all float32 or all float64 (float64:
+    flooding only, the reference's arithmetic).  flat: an existing flat buffer of that dtype
+    holding exactly those rows back to back in group order (e.g. sch_raterecover_multi's output,
+    whose row groups are views of it): used in place, nothing is copied."""
 
     def __init__(self, groups, flat=None):
         t = _lib.require_gpu()
@@ -60,8 +61,11 @@ class MixedBatch:
         self.desc = (_lib.CbDesc * max(B, 1))()
         parts, lo, co, k = [], 0, 0, 0
         self.rows = []
+        dt = groups[0][2].dtype
+        assert dt in (t.float32, t.float64), "LLRs must be float32 or float64"
+        self.dtype = _lib.F32 if dt == t.float32 else _lib.F64
         for bgn, Zc, llr in groups:
-            assert bgn in [1, 2] and find_iLS(Zc) < 8 and llr.dtype == t.float32
+            assert bgn in [1, 2] and find_iLS(Zc) < 8 and llr.dtype == dt
             K, N, Nf = code_dims(bgn, Zc)
             assert llr.dim() == 2 and llr.shape[1] == N
             for _ in range(llr.shape[0]):
@@ -74,7 +78,7 @@ class MixedBatch:
             parts.append(llr.reshape(-1))
         dev = groups[0][2].device
         if flat is not None:
-            assert flat.dtype == t.float32 and flat.is_contiguous() and flat.numel() >= lo
+            assert flat.dtype == dt and flat.is_contiguous() and flat.numel() >= lo
             self.llr = flat
         else:
             self.llr = t.cat(parts).contiguous()
@@ -105,10 +109,11 @@ class MixedBatch:
         returns the device buffers (ck flat, status (B,), iters (B,)).  rate_matched: see
         decode_mixed."""
         t = _lib.torch()
+        assert schedule != "layered" or self.dtype == _lib.F32, "the layered kernel is float32"
         host, dev = self._plan(schedule)
         with t.cuda.device(self.llr.device):
             _lib.check(_lib.lib().ldpc5g_decode_ms_mixed_plan(
-                _lib.ptr(dev), _lib.ptr(host), _lib.ptr(self.llr), _lib.F32, _lib.ptr(self.ck),
+                _lib.ptr(dev), _lib.ptr(host), _lib.ptr(self.llr), self.dtype, _lib.ptr(self.ck),
                 _lib.ptr(self.status), _lib.ptr(self.iters), int(L), float(alpha), float(beta),
                 _lib.LAYERED if schedule == "layered" else _lib.FLOODING,
                 _lib.RATE_MATCHED if rate_matched else 0, _lib.stream_ptr(self.llr.device)))

@@ -106,13 +106,16 @@ def _world(group):
     return 1, 0
 
 
-def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="layered",
+def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="flooding",
                               n_total=None, decode_fn=None, pack_fn=None, unpack_fn=None,
                               group=None, dst=0, timing=None):
     """Decode this rank's shard of a codeblock batch and gather the results to rank `dst`.
 
     llr: this rank's (n_local, N) LLR rows (device tensor), or the full (n_total, N) batch, in
          which case the rank slices its own range.
+    schedule: "flooding" (default) decodes in the reference's schedule — with float64 LLRs its
+         arithmetic too, bit-identical to nr_decode_ldpc (nr_ldpc_decode.py:11-143); "layered" is
+         the float32 perf kernel.
     Returns on rank dst: (info bits (n_total, K) int8, status (n_total,) uint8,
     iters (n_total,) int32) on dst's device; None on other ranks.  `timing` (dict) receives
     decode_s / gather_s measured on this rank (synchronised wall clock)."""
@@ -168,15 +171,19 @@ def decode_codeblocks_sharded(llr, Zc, bgn, L, alpha=1.0, beta=0.0, schedule="la
     return out
 
 
-def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule="layered",
+def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedule="flooding",
                        T_total=None, decode_fn=None, pack_fn=None, unpack_fn=None, group=None,
-                       dst=0, timing=None):
+                       dst=0, timing=None, dn_dtype=None):
     """Config 5 shape: whole transport blocks round robin across ranks (every TB's CRC stays
     rank-local), each rank running the GPU DL-SCH receive chain (sch_decode_batch: rate recovery,
     LDPC decode, CB / TB CRCs) on its TBs; (tb_ok, tbblk) records gathered to `dst`.
 
     llr: this rank's (T_local, G) LLR rows in round-robin order (TB rank, rank + world, ...), or
          the full (T_total, G) batch (then the rank takes its TBs).
+    schedule: "flooding" (default: float64 rate recovery and decoding for float64 LLRs, or with
+         dn_dtype float64 — DLSCHDecode's arithmetic) or "layered" (float32 perf kernel).
+    dn_dtype: the rate-recovered rows' dtype (sch_decode_batch; None: float32 for layered, the
+         LLRs' dtype for flooding).
     Returns on dst: (tb_ok (T_total,) uint8, tbblk (T_total, B) int8 — TB bits then CRC) in TB
     order; None elsewhere."""
     import torch
@@ -195,7 +202,7 @@ def decode_tbs_sharded(llr, cfg, L, algo="min-sum", alpha=1.0, beta=0.0, schedul
         from .sch import sch_decode_batch
 
         def decode_fn(x):
-            r = sch_decode_batch(x, cfg, L, algo, alpha, beta, schedule)
+            r = sch_decode_batch(x, cfg, L, algo, alpha, beta, schedule, dn_dtype=dn_dtype)
             return r.tb_ok, r.tbblk
     pack_fn = pack_fn or pack_records
     unpack_fn = unpack_fn or unpack_records

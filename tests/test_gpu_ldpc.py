@@ -307,13 +307,21 @@ def test_decode_split_kernel_two_processes(torch):
     codeblocks = 216 workgroups per launch (two launches cannot be resident together): parts are
     taken by arrival ticket, so both finish, every repetition equal to the first
     (tools/split_mp_probe.py; the children are new interpreters, started under a time limit)."""
+    import signal
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "split_mp_probe.py"), "2", "300"],
-                       capture_output=True, text=True, timeout=150)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert r.stdout.count("mismatches 0") == 2, r.stdout
+    # a session of its own: on the time limit the whole group (the probe AND its GPU children) dies
+    p = subprocess.Popen([sys.executable, os.path.join(root, "tools", "split_mp_probe.py"), "2", "300"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=150)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        raise
+    assert p.returncode == 0, out[-2000:] + err[-2000:]
+    assert out.count("mismatches 0") == 2, out
 
 
 def test_decode_ldpc_full_length(torch, dec):
@@ -553,12 +561,16 @@ def test_config1_layered_vs_oracle(torch, dec):
     assert st[ref_ok].all() and np.array_equal(ck[ref_ok], d["ck"][ref_ok])
 
 
-@pytest.mark.parametrize("schedule", ["layered", "flooding"])
-def test_mixed_batch_rate_matched_vs_oracle(torch, schedule):
+@pytest.mark.parametrize("schedule,dtype,rm", [("layered", "float32", False), ("flooding", "float32", False),
+                                               ("flooding", "float64", False), ("flooding", "float64", True)])
+def test_mixed_batch_rate_matched_vs_oracle(torch, schedule, dtype, rm):
     """BASELINE config 4 inputs as the bench builds them: 12 (Zc, BG) groups, each rate-matched
     on the GPU with its own (Qm, rv, E) (fillers, punctured zeros, repetitions), BPSK + AWGN,
-    rate-recovered; decoded by MixedBatch (plan built once, asynchronous launches, called twice)
-    and compared group by group with the oracle (OMS beta=0.5, L=8)."""
+    rate-recovered (float32 rows, or float64 rows: the reference's precision, nr_ldpc_raterecover.py
+    :62); decoded by MixedBatch (plan built once, asynchronous launches, called twice; rm: the
+    LDPC5G_RATE_MATCHED variant that skips dead extension rows, what the bench's config-4
+    reference-precision line runs) and compared group by group with the oracle (OMS beta=0.5,
+    L=8; float64 flooding = the reference's decode_ldpc)."""
     from python_5gtoolbox_amd.ldpc_info import code_dims
     from python_5gtoolbox_amd.nr_ldpc_decode_mixed import MixedBatch
     from python_5gtoolbox_amd.sch import cfg_from_codeblocks, sch_ratematch_batch, sch_raterecover_batch
@@ -580,17 +592,19 @@ def test_mixed_batch_rate_matched_vs_oracle(torch, schedule):
             gs = sch_ratematch_batch(ck, cfg, 1)
             y = (1 - 2 * gs.float()) + 0.9 * torch.randn(gs.shape, device="cuda", generator=g)
             llr = (2 * y / 0.81).contiguous()
-            dn = sch_raterecover_batch(llr, cfg, dn_dtype=torch.float32).clone()
+            if dtype == "float64":
+                llr = llr.double()
+            dn = sch_raterecover_batch(llr, cfg, dn_dtype=getattr(torch, dtype)).clone()
             groups.append((bg, Zc, dn))
     mb = MixedBatch(groups)
     for _ in range(2):
-        ck, st, it = mb.decode(8, 1.0, 0.5, schedule)
+        ck, st, it = mb.decode(8, 1.0, 0.5, schedule, rm)
     ck, st, it = ck.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
     k = 0
     for bg, Zc, dn in groups:
         x = dn.cpu().numpy()
         ref = (O.decode_layered(x, Zc, bg, 8, 1.0, 0.5) if schedule == "layered"
-               else O.decode_flooding(x, Zc, bg, 8, 1.0, 0.5, np.float32))
+               else O.decode_flooding(x, Zc, bg, 8, 1.0, 0.5, x.dtype.type))
         for r in range(x.shape[0]):
             co, nf = mb.rows[k]
             assert np.array_equal(ck[co:co + nf], ref[0][r]), (bg, Zc, r)

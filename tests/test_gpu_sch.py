@@ -197,6 +197,13 @@ def test_raterecover_stage_paths_vs_oracle(torch, sch, args):
             exp = np.where((ref == 0) | (hv == 0), ref + hv, (ref + hv) / 2.0).astype(out.dtype)
             outh = sch.sch_raterecover_batch(x, cfg, harq_in=h, dn_dtype=tout).cpu().numpy()
             assert np.array_equal(outh, exp), (tin, tout, "harq")
+            # in place: the HARQ input is the workspace's own output row (a previous llr_dn
+            # passed back with a reused workspace)
+            ws = sch.SchWorkspace(cfg, T, x.device)
+            buf = ws.dn_buf(tout, cfg)
+            buf.copy_(h)
+            outi = sch.sch_raterecover_batch(x, cfg, harq_in=buf, dn_dtype=tout, ws=ws).cpu().numpy()
+            assert np.array_equal(outi, exp), (tin, tout, "harq in place")
 
 
 # ------------------------------------------------------------------------------ decode chain

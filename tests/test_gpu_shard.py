@@ -44,25 +44,34 @@ def test_pack_unpack_records_vs_numpy(torch, nbits, offset):
     assert np.array_equal(it2[1::2].cpu().numpy(), it.cpu().numpy())
 
 
-def test_sharded_codeblock_decode_world1(torch):
+@pytest.mark.parametrize("schedule,dtype", [("layered", np.float32), ("flooding", np.float64)])
+def test_sharded_codeblock_decode_world1(torch, schedule, dtype):
     """decode_codeblocks_sharded on one GPU: decode -> pack records -> unpack == the plain batched
-    decode (info bits, status, iterations)."""
+    decode (info bits, status, iterations); float64 flooding (the default schedule, the
+    reference's arithmetic) also == the oracle's float64 decode_ldpc."""
     from python_5gtoolbox_amd.nr_ldpc_decode import nr_decode_ldpc_batch
     from python_5gtoolbox_amd.shard import decode_codeblocks_sharded
     rng = np.random.default_rng(1)
     bg, Zc, B = 1, 384, 64
     ck = rng.integers(0, 2, (B, 22 * Zc)).astype(np.int8)
-    llr = torch.from_numpy(O.bpsk_awgn_llr(O.encode(ck, bg), 0.5, rng).astype(np.float32)).cuda()
+    x = O.bpsk_awgn_llr(O.encode(ck, bg), 0.5, rng).astype(dtype)
+    llr = torch.from_numpy(x).cuda()
     timing = {}
-    info, st, it = decode_codeblocks_sharded(llr, Zc, bg, 8, 0.75, 0.0, "layered", timing=timing)
-    rck, rst, rit = nr_decode_ldpc_batch(llr, Zc, bg, 8, "min-sum", 0.75, 0.0, "layered")
+    info, st, it = decode_codeblocks_sharded(llr, Zc, bg, 8, 0.75, 0.0, schedule, timing=timing)
+    rck, rst, rit = nr_decode_ldpc_batch(llr, Zc, bg, 8, "min-sum", 0.75, 0.0, schedule)
     assert torch.equal(info, rck[:, :22 * Zc]) and torch.equal(st, rst) and torch.equal(it, rit)
     assert timing["gather_bytes"] == B * (1056 + 5)
+    if dtype == np.float64:
+        oc, os_, oi = O.decode_flooding(x[:8], Zc, bg, 8, 0.75, 0.0, np.float64)
+        assert np.array_equal(info[:8].cpu().numpy(), oc[:, :22 * Zc])
+        assert np.array_equal(st[:8].cpu().numpy().astype(bool), os_) and np.array_equal(it[:8].cpu().numpy(), oi)
 
 
-def test_sharded_tb_decode_world1(torch):
+@pytest.mark.parametrize("schedule", ["layered", "flooding"])
+def test_sharded_tb_decode_world1(torch, schedule):
     """decode_tbs_sharded on one GPU over a 3-TB DL-SCH batch: the gathered (crc_ok, tbblk) equal
-    sch_decode_batch's and carry the transmitted bits."""
+    sch_decode_batch's and carry the transmitted bits (flooding: float64 rate recovery + float64
+    flooding, DLSCHDecode's arithmetic)."""
     from python_5gtoolbox_amd import sch
     from python_5gtoolbox_amd.shard import decode_tbs_sharded
     A, Qm, R, NL, rv, G = 30000, 2, 500, 1, 0, 2 * 40000
@@ -72,7 +81,9 @@ def test_sharded_tb_decode_world1(torch):
     tb = torch.randint(0, 2, (3, A), dtype=torch.int8, device="cuda", generator=g)
     bits = sch.sch_encode_batch(tb, cfg).contiguous()
     llr = (8.0 * (1 - 2 * bits.float())).contiguous()
-    ok, tbblk = decode_tbs_sharded(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered")
-    r = sch.sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, "layered")
+    dn = torch.float64 if schedule == "flooding" else None
+    ok, tbblk = decode_tbs_sharded(llr, cfg, 8, "min-sum", 0.75, 0.0, schedule, dn_dtype=dn)
+    r = sch.sch_decode_batch(llr, cfg, 8, "min-sum", 0.75, 0.0, schedule, dn_dtype=dn)
+    assert r.llr_dn.dtype == (torch.float64 if schedule == "flooding" else torch.float32)
     assert torch.equal(ok, r.tb_ok) and torch.equal(tbblk, r.tbblk)
     assert ok.cpu().numpy().all() and torch.equal(tbblk[:, :A], tb)

@@ -14,6 +14,16 @@ import torch.multiprocessing as mp
 from python_5gtoolbox_amd.shard import shard_bounds, shard_round_robin
 
 
+def test_sharded_defaults_are_the_reference_schedule():
+    """Both sharded entry points decode in the reference's schedule unless asked otherwise
+    (float64 flooding for float64 LLRs: nr_ldpc_decode.py:51-143, nr_dlsch_decode.py:62-106)."""
+    import inspect
+    from python_5gtoolbox_amd.shard import decode_codeblocks_sharded, decode_tbs_sharded
+    for f in (decode_codeblocks_sharded, decode_tbs_sharded):
+        assert inspect.signature(f).parameters["schedule"].default == "flooding"
+    assert inspect.signature(decode_tbs_sharded).parameters["dn_dtype"].default is None
+
+
 def test_shard_bounds_cover_exactly():
     for n in [0, 1, 7, 4096, 4097]:
         for w in [1, 2, 3, 8]:
@@ -81,6 +91,15 @@ def _worker(rank, world, port, q):
         res = decode_codeblocks_sharded(torch.from_numpy(llr), Zc, bg, 8, 0.75, 0.0,
                                         decode_fn=dec, pack_fn=np_pack, unpack_fn=np_unpack,
                                         timing=timing)
+        # the reference's precision: float64 LLRs through float64 flooding (the default schedule)
+        llr64 = llr.astype(np.float64) * 1.37
+
+        def dec64(x):
+            assert x.dtype == torch.float64
+            c, s, i = O.decode_flooding(x.numpy(), Zc, bg, 8, 0.75, 0.0, np.float64)
+            return torch.from_numpy(c), torch.from_numpy(s.astype(np.uint8)), torch.from_numpy(i)
+        res64 = decode_codeblocks_sharded(torch.from_numpy(llr64), Zc, bg, 8, 0.75, 0.0,
+                                          decode_fn=dec64, pack_fn=np_pack, unpack_fn=np_unpack)
         # transport blocks round robin: TB i decodes to bits i, i+1, ... and CRC flag i % 2 == 0
         T, nb = 5, 37
 
@@ -121,6 +140,10 @@ def _worker(rank, world, port, q):
                 else:
                     ok &= tb3 is None
         if rank == 0:
+            fc, fs, fi = O.decode_flooding(llr64, Zc, bg, 8, 0.75, 0.0, np.float64)
+            ok &= (np.array_equal(res64[0].numpy(), fc[:, :10 * Zc])
+                   and np.array_equal(res64[1].numpy().astype(bool), fs)
+                   and np.array_equal(res64[2].numpy(), fi))
             rc, rs, ri = O.decode_layered(llr, Zc, bg, 8, 0.75, 0.0)
             ok &= (np.array_equal(res[0].numpy(), rc[:, :10 * Zc])
                    and np.array_equal(res[1].numpy().astype(bool), rs)
@@ -129,7 +152,7 @@ def _worker(rank, world, port, q):
                    and np.array_equal(tb[1].numpy(), exp_bits)
                    and timing["gather_bytes"] == world * -(-B // world) * (17 + 5))
         else:
-            ok &= res is None and tb is None
+            ok &= res is None and tb is None and res64 is None
         q.put(bool(ok))
     finally:
         dist.destroy_process_group()

@@ -44,9 +44,12 @@ def main():
         sys.exit(child(int(sys.argv[2]), int(sys.argv[3])))
     procs = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+    # the children stay in this process's group: a caller that starts this probe in a session of
+    # its own (tests/test_gpu_ldpc.py) kills them all with it on a time limit
     ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", str(11 + k), str(reps)],
                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
           for k in range(procs)]
+    deadline = time.time() + 120
     try:
         for p in ps:   # every child warmed up, then all go together
             line = p.stdout.readline()
@@ -54,12 +57,16 @@ def main():
         for p in ps:
             p.stdin.write("go\n")
             p.stdin.flush()
+        rc = []
         for p in ps:
-            print(p.stdout.read().strip(), flush=True)
-        rc = [p.wait(timeout=100) for p in ps]
+            out, _ = p.communicate(timeout=max(1.0, deadline - time.time()))
+            print(out.strip(), flush=True)
+            rc.append(p.returncode)
     except (subprocess.TimeoutExpired, AssertionError):
         for p in ps:
             p.kill()
+        for p in ps:
+            p.wait()
         raise
     print("exit codes", rc, flush=True)
     sys.exit(max(rc))
