@@ -42,7 +42,10 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_latest.json")
 # compile-time lifting size, 384 for the Zc = 384 kernels, 0 for the runtime-Zc ones)
 DEC_KERNEL = {"layered": "void ldpc_dec_kernel_l<1, float, true, false, false, 384>",
               "flooding": "void ldpc_flood_kernel<1, float, false, 2, 384, false, 384>"}
-DEC64_KERNEL = "void ldpc_flood_kernel<1, double, false, 2, 384, false, 384>"
+# the float64 Zc = 384 batches run the frame kernel (ldpc5g_dec_frame.h: <BG, OFS, DEAD>)
+DEC64_KERNEL = "void ldpc_frame_kernel<1, false, false>"
+BP_KERNEL = "void ldpc_bp_kernel<1>"
+BF_KERNEL = "void ldpc_bf_kernel<1, double>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
 
@@ -1170,14 +1173,33 @@ def main():
                            lambda: D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0), nb, 1)
             _, stb, itb = D.nr_decode_ldpc_batch(x64, ZC, BG, args.L, algo, 1.0, 0.0)
             line = {}
+            launch_s = eb / nb
+            kern = BP_KERNEL if algo == "BP" else BF_KERNEL
+            insts = pmc_valu_insts(kern) if Bb == 1024 else None
+            if insts:
+                # the executed-instruction roofline: VALU lane-ops issued / the full-rate peak and
+                # (BP: mostly float64 arithmetic) the f64 issue ceiling
+                lane_ops = insts * 64 / launch_s / 1e12
+                line["valu"] = {"bound": "valu", "achieved": round(lane_ops, 3), "unit": "T lane-op/s",
+                                "peak": round(VALU_PEAK_TLANE, 1), "frac": round(lane_ops / VALU_PEAK_TLANE, 4),
+                                "f64_issue_ceiling": round(VALU_PEAK_TLANE / 2, 1),
+                                "frac_of_f64_ceiling": round(lane_ops / (VALU_PEAK_TLANE / 2), 4),
+                                "valu_insts_per_edge_update": round(
+                                    insts * 64 / (float(itb.sum().item()) * EDGES), 2),
+                                "kernel": kern,
+                                "source": "SQ_INSTS_VALU per 1024-codeblock launch, profiles/pmc_latest.json"}
+            if algo == "BF":
+                # hard decisions live in LDS: the HBM side is the float64 LLRs in and the decisions
+                # out once per codeblock
+                line["roofline"] = hbm_line(Bb * (N_TX * 8 + N_FULL + 5), launch_s * 1e3)
             if algo == "BP":
                 # the per-edge messages live in a device scratch: each iteration reads and writes
                 # every edge's float64 message once (16 B per edge-update), plus the LLRs in and
                 # the decisions out once per codeblock
                 it_sum = int(itb.sum().item())
                 alg = it_sum * EDGES * 16 + Bb * (N_TX * 8 + N_FULL)
-                line = {"roofline": hbm_line(alg, eb / nb * 1e3),
-                        "edge_updates_per_s": round(it_sum * EDGES / (eb / nb), 1)}
+                line.update({"roofline": hbm_line(alg, eb / nb * 1e3),
+                             "edge_updates_per_s": round(it_sum * EDGES / (eb / nb), 1)})
             ex[f"{algo.lower()}_decode"] = {
                 "codeblocks_per_call": Bb, "codeblocks_per_s": round(Bb * world * nb / wb, 1), **line,
                 "launch_ms": round(eb / nb * 1e3, 4), "mean_iterations": round(itb.float().mean().item(), 3),

@@ -36,8 +36,8 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         if (LDPC5G_FLOOD_FRAME && Zc == kFrZ)
-            return bgn == 1 ? launch_frame_t<1>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st)
-                            : launch_frame_t<2>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
+            return bgn == 1 ? launch_frame_t<1, false>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st)
+                            : launch_frame_t<2, false>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
@@ -55,7 +55,7 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
-            return launch_frame_t<1>(p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
+            return launch_frame_t<1, false>(p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
         if (zc384 && bgn == 1)
             return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)

@@ -243,6 +243,38 @@ def test_decode_z384_kernels_vs_oracle(torch, dec, schedule, dtype, rm, bg):
         assert np.array_equal(g, r)
 
 
+@pytest.mark.parametrize("bg", [1, 2])
+@pytest.mark.parametrize("pattern", ["ties", "dead_rows"])
+@pytest.mark.parametrize("rm", [False, True])
+def test_decode_frame_kernel_edge_cases(torch, dec, bg, pattern, rm):
+    """The float64 Zc = 384 frame kernel (ldpc5g_dec_frame.h: per-row thread frames, column 0 / 1
+    sums in registers, hand-offs through the dead LDS image of columns 0 / 1) on inputs that stress
+    its exactness arguments, vs the oracle's float64 decode_ldpc: "ties" — integer LLRs in [-3, 3]
+    with +0.0 and -0.0 entries (equal magnitudes, zero messages, zero sums, -0.0 in iteration 0);
+    "dead_rows" — the extension columns of BG1's hand-off rows 4, 15, 19 (and BG2's rows 4, 10,
+    19) plus the last 12 never transmitted, so with rm (LDPC5G_RATE_MATCHED) whole rows and row
+    groups are skipped.  NMS (alpha .75) and OMS (beta .5), 32 codeblocks (the batch kernel)."""
+    rng = np.random.default_rng(3 + bg + 10 * rm + (pattern == "ties"))
+    Zc, B = 384, 32
+    kb = 22 if bg == 1 else 10
+    ck = rng.integers(0, 2, (B, kb * Zc)).astype(np.int8)
+    dn = O.encode(ck, bg)
+    if pattern == "ties":
+        llr = ((1 - 2 * dn) * rng.integers(0, 4, dn.shape) + rng.integers(-1, 2, dn.shape)).astype(np.float64)
+        llr[:, ::17] = -0.0
+        llr[:, 5::23] = 0.0
+    else:
+        llr = 2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 0.9) / 0.81
+        for i in ((4, 15, 19) if bg == 1 else (4, 10, 19)):   # ext column of row i: kb + i - 2
+            llr[:, (kb + i - 2) * Zc:(kb + i - 1) * Zc] = 0.0
+        llr[:, -12 * Zc:] = 0.0
+    for alpha, beta in ((0.75, 0.0), (1.0, 0.5)):
+        got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 8, "min-sum", alpha, beta, "flooding", rate_matched=rm)
+        ref = O.decode_flooding(llr, Zc, bg, 8, alpha, beta, np.float64)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r), (alpha, beta)
+
+
 @pytest.mark.parametrize("bg,Zc,B", [(1, 384, 1), (2, 384, 1), (1, 384, 7), (1, 64, 1), (1, 96, 2),
                                      (2, 72, 1), (2, 176, 3), (1, 208, 1), (2, 384, 8),
                                      # two chunks per wave (R = 2): more codeblocks than R = 1 fits

@@ -5,6 +5,10 @@
 
 #include "ldpc5g_dec_frame.h"
 
+#ifndef FRDEV_DEAD
+#define FRDEV_DEAD false   // true: the LDPC5G_RATE_MATCHED instantiation
+#endif
+
 namespace ldpc5g_impl {
 int fail(int code, const char* fmt, ...) {
     va_list ap;
@@ -24,8 +28,8 @@ extern "C" int fdev_decode(const double* llr, int8_t* ck, uint8_t* status, int32
     using namespace ldpc5g_impl;
     if (Zc != kFrZ) return LDPC5G_EZC;
     constexpr size_t lds = (size_t)kFrPlan<1>.bytes;
-    if (int rc = set_lds_once<ldpc_frame_kernel<1, false>>(lds)) return rc;
-    auto kern = ldpc_frame_kernel<1, false>;
+    if (int rc = set_lds_once<ldpc_frame_kernel<1, false, FRDEV_DEAD>>(lds)) return rc;
+    auto kern = ldpc_frame_kernel<1, false, FRDEV_DEAD>;
     hipLaunchKernelGGL(kern, dim3(B), dim3(kFrThreads), lds, st, llr, ck, status, iters,
                        (int64_t)ldl, (int64_t)ldc, L, alpha, 0.0, 2, (const DecWork*)nullptr, (const CbRef*)nullptr);
     return check_hip(hipGetLastError(), "ldpc_frame_kernel launch");

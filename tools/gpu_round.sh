@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, smoke, bench, rocprof kernel trace, encoder A/B probes and
 # PMC counter passes.  Usage (from the repo root, via gpurun):  bash tools/gpu_round.sh TAG [steps]
-#   steps: comma list of {tests,smoke,bench,trace,rehearse,probe,ab,pmc}; default tests,smoke,bench,trace,probe,pmc.
+#   steps: comma list of {tests,smoke,bench,trace,rehearse,probe,ab,pmc,calib}; default tests,smoke,bench,trace,probe,pmc.
 # Every GPU step has its own time limit.  A test FAILURE (pytest rc 1) does not stop the script;
 # a crash, abort or time limit (any other non-zero rc) ends it at once.
 set -uo pipefail
@@ -103,10 +103,45 @@ if has pmc; then
     i=$((i + 1))
     # PMC_ARGS: the profiled program's arguments (default: the headline bench)
     timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc$i" -o run -- \
-        python -u ${PMC_ARGS:-"$ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-extras} \
+        python -u ${PMC_ARGS:-"$ROOT/tools/pmc_probe.py" 3} \
         > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || { tail -5 "$OUT/pmc$i.err"; cd "$ROOT"; die "pmc $ctr" $?; }
   done
   cd "$ROOT"
   python tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.json" && cat "$OUT/pmc_summary.json"
+fi
+if has icache; then
+  echo "[gpu_round] instruction-cache counters (tools/pmc_probe.py)"
+  cd /tmp
+  i=0
+  for ctr in "SQC_ICACHE_REQ SQC_ICACHE_MISSES" "SQC_ICACHE_HITS SQC_ICACHE_MISSES_DUPLICATE" "SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+    i=$((i + 1))
+    timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/icache$i" -o run -- \
+        python -u "$ROOT/tools/pmc_probe.py" 2 > "$OUT/icache$i.log" 2>&1 || { tail -5 "$OUT/icache$i.log"; cd "$ROOT"; die "icache $ctr" $?; }
+  done
+  cd "$ROOT"
+  mkdir -p "$OUT/icache_all" && cp -r "$OUT"/icache[0-9]* "$OUT/icache_all/" 2>/dev/null
+  python - "$OUT" <<'PY'
+import csv, glob, os, sys, collections
+out = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+for f in sorted(glob.glob(out + "/icache[0-9]*/**/*counter_collection.csv", recursive=True)):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].replace("ldpc5g_impl::", "").replace("(anonymous namespace)::", "")
+        if "ldpc" not in k:
+            continue
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+for k, v in agg.items():
+    print(k[:70], {c: f"{x:.4g}" for c, x in sorted(v.items())})
+PY
+fi
+if has calib; then
+  echo "[gpu_round] FETCH_SIZE / WRITE_SIZE calibration (tools/microbench/fetch_calib: 1 GiB per kernel)"
+  cd /tmp
+  timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
+      "$ROOT/tools/microbench/fetch_calib" > "$OUT/calib_fetch.log" 2>&1 || { tail -5 "$OUT/calib_fetch.log"; cd "$ROOT"; die "calib fetch" $?; }
+  timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o run -- \
+      "$ROOT/tools/microbench/fetch_calib" > "$OUT/calib_write.log" 2>&1 || { tail -5 "$OUT/calib_write.log"; cd "$ROOT"; die "calib write" $?; }
+  cd "$ROOT"
+  python tools/microbench/fetch_calib.py "$OUT" > "$OUT/fetch_calib.json" && cat "$OUT/fetch_calib.json"
 fi
 echo "[gpu_round] done"
