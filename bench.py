@@ -49,15 +49,17 @@ BF_KERNEL = "void ldpc_bf_kernel<1, double>"
 ENC_KERNEL = "void ldpc_enc_fast_kernel<1, true>"
 
 
-def pmc_traffic(kernel, corrected16=False):
-    """HBM bytes per launch of `kernel` (4096-codeblock batch) from the committed PMC summary,
-    or None.  corrected16: FETCH_SIZE doubled for 16-B/lane streaming loads (MI355X_MICROARCH.md
-    §HBM); the decoder's 4-B loads are uncalibrated and reported raw."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary, or None: 2 x FETCH_SIZE +
+    WRITE_SIZE.  The factor is calibrated on this GPU (profiles/r06/fetch_calib.json,
+    tools/microbench/fetch_calib.hip): streaming 1 GiB with 4-, 8- and 16-B lane loads reports
+    FETCH_SIZE = 0.50 of the bytes for all three widths, and W-byte stores WRITE_SIZE = 1.00 of them
+    (MI355X_MICROARCH.md §HBM had calibrated only the 16-B read)."""
     e = pmc_entry(kernel)
     if e is None:
         return None
     try:
-        return int(e["hbm_bytes_fetch16_corrected" if corrected16 else "hbm_bytes_raw"])
+        return int(e["hbm_bytes_fetch16_corrected"])
     except (KeyError, ValueError, TypeError):
         return None
 
@@ -902,9 +904,10 @@ def bench_perf_mode(torch, dist, world, llr, out, args, cpu_res):
                      "hbm_achieved_GBps": round(achieved, 2), "hbm_peak_GBps": HBM_PEAK_GBS,
                      "hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
                      "algorithmic_bytes_per_cb": DEC_BYTES_PER_CB,
-                     "traffic_source": "profiles/pmc_latest.json: FETCH_SIZE + WRITE_SIZE bytes "
-                                       "per 4096-CB launch (raw; FETCH includes Infinity-Cache "
-                                       "hits of the per-iteration ext-column LLR re-reads)"},
+                     "traffic_source": "profiles/pmc_latest.json: 2 x FETCH_SIZE + WRITE_SIZE bytes "
+                                       "per 4096-CB launch (factor calibrated, profiles/r06/"
+                                       "fetch_calib.json; FETCH includes Infinity-Cache hits of the "
+                                       "per-iteration ext-column LLR re-reads)"},
         "valu": valu_block(edge_rate, launch_s, DEC_KERNEL["layered"], B),
         "cpu_baseline": cpu_res,
     }
@@ -955,8 +958,9 @@ def bench_reference_precision(torch, dist, world, llr, out, args, cpu64):
                                     f"codeblock (f64 LLR in, ck, status, iters)",
                      "note": "two ceilings: the full-rate lane peak (78.6 T) and the float64 issue "
                              "ceiling (39.3 T: v_add/min/max/cmp_f64 issue at half rate on gfx950, "
-                             "profiles/r02/r02o_valu_rates_f64.txt); traffic = FETCH_SIZE + "
-                             "WRITE_SIZE per launch, profiles/pmc_latest.json"},
+                             "profiles/r02/r02o_valu_rates_f64.txt); traffic = 2 x FETCH_SIZE + "
+                             "WRITE_SIZE bytes per launch (calibrated: profiles/r06/fetch_calib.json), "
+                             "profiles/pmc_latest.json"},
         "valu": valu_block(edge_rate, launch_s, DEC64_KERNEL, B),
         "cpu_baseline": cpu64,
     }
@@ -1121,7 +1125,7 @@ def main():
                                 "roofline": {"bound": "hbm", "achieved": round(ach, 1),
                                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                              "frac": round(ach / HBM_PEAK_GBS, 4),
-                                             "traffic": pmc_traffic(ENC_KERNEL, True)
+                                             "traffic": pmc_traffic(ENC_KERNEL)
                                              if B == 4096 else None,
                                              "kernel": ENC_KERNEL,
                                              "algorithmic_bytes_per_cb": ENC_BYTES_PER_CB,

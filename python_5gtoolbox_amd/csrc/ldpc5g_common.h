@@ -187,6 +187,22 @@ int launch_flood_split(int bgn, const double* llr, int8_t* ck, uint8_t* status, 
                        int Zc, int zi, int64_t ldl, int64_t ldc, int L, double alpha, double beta,
                        int pc, hipStream_t st);
 int split_timeouts(uint32_t* count);   // codeblocks whose split decode timed out (this device)
+// float64 flooding of Zc = 384 batches: the frame kernel (ldpc5g_dec_frame.h), one translation unit
+// per (base graph, DEAD) so they compile in parallel (ldpc5g_dec_frame{1,2}{,_dead}.hip)
+constexpr int kFrameZc = 384;
+template <int BG, bool DEAD>
+int launch_frame_bg(const double* llr, int8_t* ck, uint8_t* status, int32_t* iters, int nwg, int64_t ldl,
+                    int64_t ldc, int L, double alpha, double beta, int pc, const DecWork* work,
+                    const CbRef* cbs, hipStream_t st);
+inline int launch_frame(int bgn, bool dead, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,
+                        int nwg, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
+                        const DecWork* work, const CbRef* cbs, hipStream_t st) {
+    if (bgn == 1)
+        return dead ? launch_frame_bg<1, true>(llr, ck, status, iters, nwg, ldl, ldc, L, alpha, beta, pc, work, cbs, st)
+                    : launch_frame_bg<1, false>(llr, ck, status, iters, nwg, ldl, ldc, L, alpha, beta, pc, work, cbs, st);
+    return dead ? launch_frame_bg<2, true>(llr, ck, status, iters, nwg, ldl, ldc, L, alpha, beta, pc, work, cbs, st)
+                : launch_frame_bg<2, false>(llr, ck, status, iters, nwg, ldl, ldc, L, alpha, beta, pc, work, cbs, st);
+}
 int launch_bf(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* status, int32_t* iters,
               int B, int Zc, int zi, int64_t ldl, int64_t ldc, int L, int pc, hipStream_t st);
 int launch_bp(int bgn, const double* llr, int8_t* ck, uint8_t* status, int32_t* iters,

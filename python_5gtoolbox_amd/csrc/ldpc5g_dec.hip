@@ -1,12 +1,8 @@
 // ldpc5g_dec.hip — flooding min-sum decoder instantiations (float64: the drop-in's bit-exact path;
 // float32 in ldpc5g_dec_f32.hip) and the decoder dispatch; the layered kernels live in ldpc5g_dec_l.hip.
 // Part of libldpc5g.so (MI355X, gfx950).
-#include "ldpc5g_dec_frame.h"
+#include "ldpc5g_dec_flood.h"
 
-// float64 Zc = 384 batches: the frame kernel (ldpc5g_dec_frame.h) instead of ldpc_flood_kernel
-#ifndef LDPC5G_FLOOD_FRAME
-#define LDPC5G_FLOOD_FRAME 1
-#endif
 
 namespace ldpc5g_impl {
 
@@ -35,9 +31,8 @@ int launch_dec(int bgn, int dtype, bool layered, const void* llr, int8_t* ck, ui
     if (dead) return launch_flood_dead(bgn, dtype, llr, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
-        if (LDPC5G_FLOOD_FRAME && Zc == kFrZ)
-            return bgn == 1 ? launch_frame_t<1, false>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st)
-                            : launch_frame_t<2, false>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
+        if (LDPC5G_FLOOD_FRAME && Zc == kFrameZc)
+            return launch_frame(bgn, false, p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
         return bgn == 1 ? launch_flood_t<1, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
@@ -55,9 +50,10 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
-            return launch_frame_t<1, false>(p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
-        if (zc384 && bgn == 1)
-            return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+            return launch_frame(1, false, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
+        if constexpr (!LDPC5G_FLOOD_FRAME)
+            if (zc384 && bgn == 1)
+                return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }

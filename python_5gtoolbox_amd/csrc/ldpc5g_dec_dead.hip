@@ -1,11 +1,8 @@
 // ldpc5g_dec_dead.hip — the flooding decoder's dead-extension-row variants (DEAD = true, float64
 // batch and mixed work lists), selected by LDPC5G_RATE_MATCHED: float64 here,
 // float32 in ldpc5g_dec_dead_f32.hip.  Own translation units: they compile in parallel.
-#include "ldpc5g_dec_frame.h"
+#include "ldpc5g_dec_flood.h"
 
-#ifndef LDPC5G_FLOOD_FRAME
-#define LDPC5G_FLOOD_FRAME 1   // float64 Zc = 384: the frame kernel (ldpc5g_dec_frame.h)
-#endif
 
 namespace ldpc5g_impl {
 
@@ -14,9 +11,8 @@ int launch_flood_dead(int bgn, int dtype, const void* llr, int8_t* ck, uint8_t* 
                       double alpha, double beta, int pc, hipStream_t st) {
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
-        if (LDPC5G_FLOOD_FRAME && Zc == kFrZ)
-            return bgn == 1 ? launch_frame_t<1, true>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st)
-                            : launch_frame_t<2, true>(p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
+        if (LDPC5G_FLOOD_FRAME && Zc == kFrameZc)
+            return launch_frame(bgn, true, p, ck, status, iters, B, ldl, ldc, L, alpha, beta, pc, nullptr, nullptr, st);
         return bgn == 1 ? launch_flood_t<1, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st)
                         : launch_flood_t<2, double, true>(p, ck, status, iters, B, Zc, zi, ldl, ldc, L, alpha, beta, pc, st);
     }
@@ -29,9 +25,10 @@ int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uin
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
         if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
-            return launch_frame_t<1, true>(p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
-        if (zc384 && bgn == 1)
-            return launch_flood_mixed_t<1, double, true, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
+            return launch_frame(1, true, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
+        if constexpr (!LDPC5G_FLOOD_FRAME)
+            if (zc384 && bgn == 1)
+                return launch_flood_mixed_t<1, double, true, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
         return bgn == 1 ? launch_flood_mixed_t<1, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st)
                         : launch_flood_mixed_t<2, double, true>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
     }

@@ -25,6 +25,11 @@ namespace ldpc5g_impl {
 namespace {
 
 constexpr size_t kLdsPerCU = 160 * 1024;
+// 1: float64 Zc = 384 batches run the frame kernel (ldpc5g_dec_frame.h) and this header's Zc = 384
+// float64 instantiation is not built; 0 (tools/flood_dev A/B builds): this kernel again
+#ifndef LDPC5G_FLOOD_FRAME
+#define LDPC5G_FLOOD_FRAME 1
+#endif
 #ifndef LDPC5G_FLOOD_XPRE
 #define LDPC5G_FLOOD_XPRE 4
 #endif
@@ -878,7 +883,7 @@ int launch_flood_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, in
                    int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc, hipStream_t st) {
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks
     const int G = std::min(dec_G(Zc, false), B);
-    if constexpr (flood_wtab<BG, T, kFloodNP, kFloodCS>())
+    if constexpr (flood_wtab<BG, T, kFloodNP, kFloodCS>() && !(LDPC5G_FLOOD_FRAME && std::is_same_v<T, double>))
         if (Zc == kFloodCS)   // the largest lifting size has its own kernel (zc_shift)
             return launch_flood_cfg<BG, T, kFloodNP, kFloodCS, DEAD, kFloodCS>(
                 llr, ck, status, iters, B, Zc, zi, G, ldl, ldc, L, alpha, beta, pc, st);

@@ -21,7 +21,7 @@
 namespace ldpc5g_impl {
 namespace {
 
-constexpr int kFrZ = 384;
+constexpr int kFrZ = kFrameZc;
 constexpr int kFrThreads = 2 * kFrZ;
 constexpr int kFrColB = kFrZ * 8;          // one LQ column (float64) or hand-off slot
 constexpr int kFrRowB = kFrZ * (16 + 4);   // one LDS state row: (mA, mB) pairs + sign words

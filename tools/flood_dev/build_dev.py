@@ -74,7 +74,7 @@ def make(name):
         open(p, "w").write(s)
     out = os.path.join(ROOT, "build", "fdev", name + ".so")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
-           "-shared", f"-I{ROOT}/include", f"-I{d}", *os.environ.get("FDEV_FLAGS", "").split(), *FLAGS.get(name, []),
+           "-shared", f"-I{ROOT}/include", f"-I{d}", "-DLDPC5G_FLOOD_FRAME=0", *os.environ.get("FDEV_FLAGS", "").split(), *FLAGS.get(name, []),
            os.path.join(HERE, "fdev.hip"), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     return name, r.returncode, r.stderr[-3000:]

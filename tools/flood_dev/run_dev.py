@@ -40,9 +40,13 @@ def main():
         sigma = 10 ** (-snr / 20)
         llr = (2 * ((1 - 2 * dn.double()) + sigma * torch.randn(dn.shape, device="cuda", dtype=torch.float64,
                                                                   generator=g)) / sigma ** 2).contiguous()
+        dead = int(os.environ.get("FDEV_DEADCOLS", "0"))   # the last `dead` extension columns untransmitted
+        if dead:
+            llr[:, -dead * ZC:] = 0.0
         ref = (torch.empty((B, NF), dtype=torch.int8, device="cuda"), torch.empty((B,), dtype=torch.uint8, device="cuda"),
                torch.empty((B,), dtype=torch.int32, device="cuda"))
-        prod = lambda: D.nr_decode_ldpc_batch(llr, ZC, 1, 8, "min-sum", 0.75, 0.0, "flooding", out=ref)  # noqa: E731
+        prod = lambda: D.nr_decode_ldpc_batch(llr, ZC, 1, 8, "min-sum", 0.75, 0.0, "flooding", out=ref,  # noqa: E731
+                                              rate_matched=bool(dead))
         runs = [("product", prod)]
         outs = {}
         for p, lib in libs:
