@@ -229,12 +229,14 @@ constexpr uint64_t fr_group_xmask(int g) {
 // and adds nothing in phase B (its core messages are +-0: S + (+-0) = S, since no column sum or
 // register sum is ever -0.0, and no dead row is a column's first row); a group of dead rows needs
 // no barrier.  Bit-identical to the full update.
-// The kernel's work; live_x: bit i - 4 set iff extension row i is live (DEAD only).
-template <int BG, bool OFS, bool DEAD>
+// The kernel's work.  KDEAD: the prologue also finds the live extension rows (bit i - 4 of live_x:
+// some entry of row i's LLR column is not +0.0), and a codeblock with a dead row iterates with the
+// dead-row shortcuts, one without runs the plain iterations (the shortcuts' checks cost ~15 %).
+template <int BG, bool OFS, bool KDEAD>
 __device__ __forceinline__ void frame_body(
     const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
-    const DecWork* __restrict__ work, const CbRef* __restrict__ cbs, uint64_t live_x) {
+    const DecWork* __restrict__ work, const CbRef* __restrict__ cbs) {
     using T = double;
     using P = BGT<BG>;
     constexpr int Z = kFrZ, MB = P::MB, KB = P::KB, KC = P::KC;
@@ -327,7 +329,11 @@ __device__ __forceinline__ void frame_body(
         }
     };
 
-    // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS state 0; wrap table; flags
+    // ---- load: LQ = LLRin (:94), punctured columns 0 (:43); LDS state 0; wrap table; flags.
+    // KDEAD: each thread also loads its entry of its half's extension rows (in the row's frame:
+    // together all Zc entries of every row); a wave's ballots give one word (bit p: xlist row p
+    // live) at the flags' offset 16 + 4 * wave, ORed per half after the prologue's barrier.
+    static_assert(kFrThreads / 64 * 4 + 16 <= kFrFlagB, "per-wave liveness words in the flags");
     {
         T v0[KH];
 #pragma unroll
@@ -335,11 +341,30 @@ __device__ __forceinline__ void frame_body(
             const int j = jcol(jj);
             v0[jj] = lrow[(j < pc ? 0 : j - pc) * Z + s];
         }
+        uint32_t wm = 0;
+        if constexpr (KDEAD) {
+            per_half([&](auto hc) {
+                constexpr int hh = decltype(hc)::value, NX = kFrPlan<BG>.nx[hh];
+                static_assert(NX <= 32, "one liveness word per wave");
+                T xv[NX];
+                sfor<0, NX>([&](auto xc) {
+                    constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
+                    constexpr int c = (Z - kFrPlan<BG>.off[i]) % Z;
+                    const int x = c == 0 ? s : (int)min((uint32_t)(s + c), (uint32_t)(s + c - Z));
+                    xv[decltype(xc)::value] = lrow_x[i * Z + x];
+                });
+                sfor<0, NX>([&](auto xc) {
+                    constexpr int p = decltype(xc)::value;
+                    wm |= (uint32_t)(__builtin_amdgcn_ballot_w64(FT<T>::bits(xv[p]) != 0) != 0) << p;
+                });
+            });
+        }
 #pragma unroll
         for (int jj = 0; jj < KH; ++jj) {
             const int j = jcol(jj);
             at((uint32_t)(j * kFrColB + s * 8)) = j < pc ? T(0) : v0[jj];
         }
+        if (KDEAD && (t & 63) == 0) *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.fl_b + 16 + (t >> 6) * 4) = wm;
     }
     for (int w = t; w < kFrPlan<BG>.nls * Z; w += kFrThreads) {
         V2<T> v;
@@ -351,7 +376,23 @@ __device__ __forceinline__ void frame_body(
     *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.tbl_b + t * 4) = (uint32_t)s * 8u;
     if (t == 0) *flagA = 0, *anyf = 0;
     lds_barrier();
-    auto rdead = [&](int i) -> bool { return DEAD && i >= 4 && ((live_x >> (i - 4)) & 1u) == 0; };
+    uint64_t live_x = ~0ull;
+    if constexpr (KDEAD) {
+        constexpr int NW = kFrThreads / 64, HW = Z / 64;
+        uint32_t m[2] = {0u, 0u};
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            m[w / HW] |= *(lds_u32*)(uintptr_t)(uint32_t)(kFrPlan<BG>.fl_b + 16 + w * 4);
+        live_x = 0;
+        sfor<0, 2>([&](auto hc) {
+            constexpr int hh = decltype(hc)::value;
+            const uint32_t mh = __builtin_amdgcn_readfirstlane(m[hh]);
+            sfor<0, kFrPlan<BG>.nx[hh]>([&](auto xc) {
+                constexpr int p = decltype(xc)::value;
+                live_x |= (uint64_t)((mh >> p) & 1u) << (kFrPlan<BG>.xlist[hh][p] - 4);
+            });
+        });
+    }
 
     const uint32_t sb0 = (uint32_t)s * 8u, sbw0 = sb0 - (uint32_t)(Z * 8);
     const uint32_t tz0 = (uint32_t)(kFrPlan<BG>.tbl_b + s * 4);
@@ -360,247 +401,18 @@ __device__ __forceinline__ void frame_body(
     bool active = true;
     uint64_t hdx_keep = 0;   // extension decisions of a codeblock decided by the syndrome test
     int it = 0;
-    for (; it < L; ++it) {
-        // opaque per iteration: otherwise LICM hoists hundreds of loop-invariant addresses
-        uint32_t sb = sb0, sbw = sbw0, tz = tz0;
-        int sv = s;
-        asm volatile("" : "+v"(sb));
-        asm volatile("" : "+v"(sbw));
-        asm volatile("" : "+v"(tz));
-        asm volatile("" : "+v"(sv));
-        auto rot = [&](int c) -> uint32_t { return fr_rot(sb, sbw, c); };
-        // check node of row i run by this thread: (s - off[i]) mod Zc
-        auto xpos = [&](int i) -> int {
-            const int c = (Z - kFrPlan<BG>.off[i]) % Z;
-            if (c == 0) return sv;
-            return (int)min((uint32_t)(sv + c), (uint32_t)(sv + c - Z));
-        };
-        auto llrx = [&](int i) -> T { return lrow_x[i * Z + xpos(i)]; };
-        bool fail = false;
-        uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
-
-        // ext LLR ring: slot p % XP holds the LLR of the half's ext row p, loaded XP rows ahead
-        constexpr int XP = kXPre > 0 ? kXPre : 1;
-        T xr[XP];
-        auto xload = [&](auto hc, auto pc_) {
-            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
-            if constexpr (p < kFrPlan<BG>.nx[hh]) xr[p % XP] = llrx(kFrPlan<BG>.xlist[hh][p]);
-        };
-        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202); core-edge
-        // LQ reads one edge ahead, their wrap-table offsets two ahead
-        struct RowSt {
-            T mA, mB, min1, min2;
-            uint32_t u, idxo, idx, negs;
-            bool par;
-            T ab;
-            uint32_t tb[2];
-        };
-        auto aloadt = [&](RowSt& r, auto ic, auto kc3) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k3 = decltype(kc3)::value;
-            if constexpr (k3 < d)
-                if constexpr (P::COL[e0 + k3] < KC) r.tb[k3 % 2] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k3) * 4u);
-        };
-        auto aload = [&](RowSt& r, auto ic, auto kc2) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k2 = decltype(kc2)::value;
-            if constexpr (k2 < d)
-                if constexpr (P::COL[e0 + k2] < KC) r.ab = at((uint32_t)(P::COL[e0 + k2] * kFrColB) + r.tb[k2 % 2]);
-        };
-        auto rowA = [&](auto ic) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
-            RowSt r;
-            get_state(ic, r.mA, r.mB, r.u, r.idxo);
-            r.min1 = FT<T>::inf(), r.min2 = FT<T>::inf();
-            r.idx = 0, r.negs = 0, r.par = false;
-            aloadt(r, ic, std::integral_constant<int, 0>{});
-            aloadt(r, ic, std::integral_constant<int, 1>{});
-            aload(r, ic, std::integral_constant<int, 0>{});
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
-                const T rold = xsign_v(pick(r.idxo == (uint32_t)k, r.mB, r.mA), r.u, mv);
-                asm("v_add_u32 %0, %1, %1" : "=v"(r.u) : "v"(r.u));   // u <<= 1, all-VGPR form
-                T a;
-                if constexpr (j < KC) {
-                    a = r.ab;
-                    aload(r, ic, std::integral_constant<int, k + 1>{});
-                    aloadt(r, ic, std::integral_constant<int, k + 2>{});
-                    __builtin_amdgcn_sched_barrier(0);
-                    r.par ^= a < T(0);
-                } else {
-                    constexpr int hh = kFrPlan<BG>.owner[i], p = kFrPlan<BG>.xpos[i];
-                    a = xr[p % XP] + rold;   // LQ of a degree-1 column = LLR + its only r
-                    xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});
-                    hdx |= (uint64_t)(a < T(0)) << (i - 4);
-                    r.par ^= a < T(0);
-                }
-                const T q = a - rold;
-                const T aq = fabs(q);
-                r.idx = aq < r.min1 ? (uint32_t)k : r.idx;
-                asm volatile("" : "+v"(r.idx));
-                r.negs = __builtin_amdgcn_alignbit(r.negs, FT<T>::sbits(q), 31);
-                two_min(r.min1, r.min2, aq);
-            });
-            fail |= r.par;
-            T x1 = r.min1, x2 = r.min2;
-            if constexpr (OFS) {
-                x1 = r.min1 - beta, x2 = r.min2 - beta;   // max(minv - beta, 0) (:201)
-                x1 = x1 > T(0) ? x1 : T(0), x2 = x2 > T(0) ? x2 : T(0);
-            }
-            const uint32_t sgn = 0u - (__builtin_popcount(r.negs) & 1u);   // the row's sign product
-            put_state(ic, alpha * x1, alpha * x2, r.negs ^ (sgn & ((1u << d) - 1u)), r.idx);
-        };
-        // a dead extension row: LQ_ext = 0 + r_old_ext (its syndrome bit), q_core = LQ - (+-0); the
-        // new state as the full update leaves it up to zero signs (ldpc5g_dec_flood.h rowA_dead)
-        auto rowA_dead = [&](auto ic) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
-            T mA, mB;
-            uint32_t u, idxo;
-            get_state(ic, mA, mB, u, idxo);
-            const T rext = xsign_v(pick(idxo == (uint32_t)(d - 1), mB, mA), u << (d - 1), mv);
-            constexpr int hh = kFrPlan<BG>.owner[i], p = kFrPlan<BG>.xpos[i];
-            xload(std::integral_constant<int, hh>{}, std::integral_constant<int, p + XP>{});   // keep the ring moving
-            const T ax = T(0) + rext;
-            hdx |= (uint64_t)(ax < T(0)) << (i - 4);
-            bool par = ax < T(0);
-            T mn = FT<T>::inf();
-            uint32_t sx = 0;
-            sfor<0, d>([&](auto kc) {
-                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
-                if constexpr (j < KC) {
-                    const T a = at((uint32_t)(j * kFrColB) + rot(fr_cof<BG>(i, k)));
-                    par ^= a < T(0);
-                    mn = fmin(mn, fabs(a));
-                    sx ^= FT<T>::sbits(a);
-                }
-            });
-            fail |= par;
-            T x2 = mn;
-            if constexpr (OFS) {
-                x2 = mn - beta;
-                x2 = x2 > T(0) ? x2 : T(0);
-            }
-            put_state(ic, T(0), alpha * x2, sx >> 31, (uint32_t)(d - 1));
-        };
-        if (active) {
-            per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
-            sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
-                constexpr int i = decltype(ic)::value;
-                if (h == kFrPlan<BG>.owner[i]) {
-                    if constexpr (DEAD && i >= 4) {
-                        if (rdead(i)) rowA_dead(ic);
-                        else rowA(ic);
-                    } else {
-                        rowA(ic);
-                    }
-                }
-            });
-            if (fail) *flagA = 1;
+    if constexpr (KDEAD) {
+        constexpr uint64_t all = (1ull << (MB - 4)) - 1;
+        if (live_x != all) {
+            constexpr bool DEAD = true;
+#include "ldpc5g_dec_frame_iter.h"
+        } else {
+            constexpr bool DEAD = false;
+#include "ldpc5g_dec_frame_iter.h"
         }
-        lds_barrier();
-        // ---- the syndrome of LQ_old decides (:107-114): output its hard decisions
-        if (active && *flagA == 0) {
-            hdx_keep = hdx;   // the LQ image stays frozen (no phase B) for the decisions
-            if (t == 0) status[out] = 1, iters[out] = it;
-            active = false;
-        }
-
-        // ---- phase B: Lr.sum(axis=0) in row order (:126).  Columns >= 2: ds_add into the LQ
-        // image, one barrier per group; column h: this thread's register sum S.
-        auto msg = [&](T a, T b, uint32_t u, uint32_t idx, auto kc) -> T {   // r of edge k
-            constexpr int k = decltype(kc)::value;
-            return xsign_v(pick(idx == (uint32_t)k, b, a), u << k, mv);
-        };
-        auto add_to = [&](auto ic, auto kc, T r, uint32_t ent) {   // column of edge k of row i
-            constexpr int i = decltype(ic)::value, k = decltype(kc)::value, j = P::COL[P::RS[i] + k];
-            lds_T& acc = at((uint32_t)(j * kFrColB) + ent);
-            if constexpr (kFrPlan<BG>.first_row[j] == i) acc = T(0) + r;
-            else __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-        T S = T(0);
-        // the core LLRs of the LQ update, loaded now so phase B hides their latency
-        T lf[KH];
-        if (active) {
-#pragma unroll
-            for (int jj = 0; jj < KH; ++jj) {
-                const int j = jcol(jj);
-                lf[jj] = lrow[(j < pc ? 0 : j - pc) * Z + sv];
-            }
-            // hand-offs: the other column's message of this half's rows with both columns
-            per_half([&](auto hc) {
-                constexpr int H = decltype(hc)::value;
-                sfor<0, MB>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    if constexpr (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.owner[i] == H) {
-                        if (rdead(i)) return;   // its messages are +-0: nothing to hand over
-                        constexpr int k = kFrPlan<BG>.kc[1 - H][i];
-                        T a, b;
-                        uint32_t u, idx;
-                        get_state(ic, a, b, u, idx);
-                        at((uint32_t)kFrPlan<BG>.hb(kFrPlan<BG>.ho[i]) + rot(fr_cof<BG>(i, k))) =
-                            msg(a, b, u, idx, std::integral_constant<int, k>{});
-                    }
-                });
-            });
-        }
-        sfor<0, kFrPlan<BG>.ng>([&](auto gc) {
-            constexpr int g = decltype(gc)::value;
-            constexpr uint64_t gx = fr_group_xmask<BG>(g);
-            const bool gdead = DEAD && gx != 0 && (live_x & gx) == 0;   // adds nothing: no barrier
-            if (active && !gdead) {
-                per_half([&](auto hc) {
-                    constexpr int H = decltype(hc)::value;
-                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {
-                        constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
-                        if (rdead(i)) return;   // +-0 messages: no add changes a sum
-                        if constexpr (kFrPlan<BG>.lds[i]) {
-                            // both halves: column H's message and this half's share of the edges of
-                            // columns >= 2, from the state at check node (s - Pf) mod Zc, Pf = V(i, H)
-                            constexpr int Pf = fr_pf<BG>(i, H);
-                            T a, b;
-                            uint32_t u, idx;
-                            lds_get(ic, rot((Z - Pf) % Z), a, b, u, idx);
-                            sfor<0, d>([&](auto kc) {
-                                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
-                                if constexpr (j == H) {
-                                    S = S + xsign_v(pick(idx == (uint32_t)k, b, a), u, mv);
-                                } else if constexpr (fr_item<BG>(H, i, k)) {
-                                    add_to(ic, kc, xsign_v(pick(idx == (uint32_t)k, b, a), u, mv),
-                                           rot((fr_sft<BG>(i, k) - Pf + Z) % Z));
-                                }
-                                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));   // u <<= 1
-                            });
-                        } else if constexpr (kFrPlan<BG>.owner[i] == H) {
-                            // this half's VGPR row in frame H: column H's entry is this thread's own
-                            T a, b;
-                            uint32_t u, idx;
-                            get_state(ic, a, b, u, idx);
-                            sfor<0, d>([&](auto kc) {
-                                constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
-                                if constexpr (j == H) {
-                                    S = S + xsign_v(pick(idx == (uint32_t)k, b, a), u, mv);
-                                } else if constexpr (j >= 2 && j < KC) {
-                                    add_to(ic, kc, xsign_v(pick(idx == (uint32_t)k, b, a), u, mv), rot(fr_cof<BG>(i, k)));
-                                }
-                                asm("v_add_u32 %0, %1, %1" : "=v"(u) : "v"(u));
-                            });
-                        } else if constexpr (kFrPlan<BG>.ho[i] >= 0 && kFrPlan<BG>.kc[H][i] >= 0) {
-                            S = S + at((uint32_t)kFrPlan<BG>.hb(kFrPlan<BG>.ho[i]) + sb);   // the owner's hand-off
-                        }
-                    });
-                });
-            }
-            if (!gdead) lds_barrier();
-        });
-        // ---- LQ = LLRin + sum (:126) for the own entries
-        if (active) {
-#pragma unroll
-            for (int jj = 0; jj < KH; ++jj) {
-                const int j = jcol(jj);
-                lds_T& x = at((uint32_t)(j * kFrColB) + sb);
-                x = (j < pc ? T(0) : lf[jj]) + (jj == 0 ? S : x);   // punctured columns: LLR 0 (:43)
-            }
-        }
-        if (t == 0) *flagA = 0;   // read before the phase-B barriers
-        if (!block_any(active)) break;
+    } else {
+        constexpr bool DEAD = false;
+#include "ldpc5g_dec_frame_iter.h"
     }
 
     // ---- iterations exhausted: ck = (LQ <= 0), status = syndrome == 0 (:133-143)
@@ -684,58 +496,13 @@ __device__ __forceinline__ void frame_body(
     ck_store_staged(NFZ, 1, [&](int) -> int8_t* { return crow; }, slow, t, kFrThreads);
 }
 
-// Extension rows (bits i - 4) whose LLR is not +0.0 in some entry of the workgroup's codeblock:
-// every thread looks at its own entry of each of its half's extension rows, in the row's frame
-// (together a permutation of all Zc entries per row).  LDS words at the flags' offset 16.
-template <int BG>
-__device__ __forceinline__ uint64_t frame_live_rows(const double* __restrict__ llr, int64_t ldl, int pc,
-                                                    const DecWork* __restrict__ work,
-                                                    const CbRef* __restrict__ cbs) {
-    using P = BGT<BG>;
-    constexpr int Z = kFrZ;
-    const int t = threadIdx.x;
-    const int h = __builtin_amdgcn_readfirstlane(t / Z);
-    const int s = t - h * Z;
-    const double* lrow = work ? llr + cbs[work[blockIdx.x].first].llr_off : llr + (int64_t)blockIdx.x * ldl;
-    const double* lrow_x = lrow + (P::KB - pc) * Z;
-    extern __shared__ __align__(16) unsigned char smem[];
-    uint32_t* livew = (uint32_t*)(smem + kFrPlan<BG>.fl_b + 16);   // (derived from smem: an LDS pointer)
-    if (t == 0) livew[0] = 0u, livew[1] = 0u;
-    lds_barrier();
-    uint64_t nzx = 0;
-    sfor<0, 2>([&](auto hc) {
-        constexpr int hh = decltype(hc)::value;
-        if (h == hh)
-            sfor<0, kFrPlan<BG>.nx[hh]>([&](auto xc) {
-                constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
-                constexpr int c = (Z - kFrPlan<BG>.off[i]) % Z;
-                const int x = c == 0 ? s : (int)min((uint32_t)(s + c), (uint32_t)(s + c - Z));
-                nzx |= (uint64_t)(FT<double>::bits(lrow_x[i * Z + x]) != 0) << (i - 4);
-            });
-    });
-    if (nzx & 0xffffffffu) atomicOr(&livew[0], (uint32_t)nzx);
-    if (nzx >> 32) atomicOr(&livew[1], (uint32_t)(nzx >> 32));
-    lds_barrier();
-    return ((uint64_t)__builtin_amdgcn_readfirstlane(livew[1]) << 32) |
-           (uint64_t)__builtin_amdgcn_readfirstlane(livew[0]);
-}
-
-// DEAD: a workgroup whose codeblock has no dead row runs the plain body (the dead-row checks cost
-// the full decode ~15 %: 3.25 -> 3.75 ms per 4096 BG1 codeblocks)
+// DEAD: rate-matched input (dead extension rows found per codeblock in frame_body's prologue)
 template <int BG, bool OFS, bool DEAD>
 __global__ __launch_bounds__(kFrThreads) __attribute__((amdgpu_waves_per_eu(3))) void ldpc_frame_kernel(
     const double* __restrict__ llr, int8_t* __restrict__ ck, uint8_t* __restrict__ status,
     int32_t* __restrict__ iters, int64_t ldl, int64_t ldc, int L, double alpha, double beta, int pc,
     const DecWork* __restrict__ work, const CbRef* __restrict__ cbs) {
-    if constexpr (DEAD) {
-        constexpr uint64_t all = (1ull << (BGT<BG>::MB - 4)) - 1;
-        const uint64_t live = frame_live_rows<BG>(llr, ldl, pc, work, cbs);
-        if (live != all) {
-            frame_body<BG, OFS, true>(llr, ck, status, iters, ldl, ldc, L, alpha, beta, pc, work, cbs, live);
-            return;
-        }
-    }
-    frame_body<BG, OFS, false>(llr, ck, status, iters, ldl, ldc, L, alpha, beta, pc, work, cbs, ~0ull);
+    frame_body<BG, OFS, DEAD>(llr, ck, status, iters, ldl, ldc, L, alpha, beta, pc, work, cbs);
 }
 
 template <int BG, bool DEAD>

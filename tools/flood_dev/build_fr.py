@@ -33,14 +33,8 @@ PATCHES = {
     "nobar": [("            lds_barrier();\n        });\n        }\n", "        });\n        }\n")],
     "plain": [("            else __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);",
                "            else acc = r;")],
-    # DEAD kernel probes: the liveness pass skipped (opaque all-live mask, both bodies kept) /
-    # the liveness pass kept but the plain body always
-    "nolive": [("        const uint64_t live = frame_live_rows<BG>(llr, ldl, pc, work, cbs);",
-                "        uint64_t live = all;\n        asm volatile(\"\" : \"+s\"(live));")],
-    "onlyplain": [("        if (live != all) {", "        if (live == 12345) {")],
-    "checklive": [("            frame_body<BG, OFS, true>(llr, ck, status, iters, ldl, ldc, L, alpha, beta, pc, work, cbs, live);",
-                   "            frame_body<BG, OFS, true>(llr, ck, status, iters, ldl, ldc, L, alpha, beta, pc, work, cbs, live);\n"
-                   "            if (threadIdx.x == 0) iters[blockIdx.x] = 1000 + __builtin_popcountll(live);")],
+    # DEAD kernel probe: the prologue's liveness loads kept, the plain iterations always
+    "onlyplain": [("        if (live_x != all) {", "        if (live_x == 12345) {")],
 }
 
 
