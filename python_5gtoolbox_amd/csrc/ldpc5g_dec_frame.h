@@ -188,6 +188,44 @@ template <int BG>
 constexpr FramePlan<BG> kFrPlan{};
 static_assert(kFrPlan<1>.ok && kFrPlan<2>.ok, "frame plan");
 
+// The core-edge stream of each half: the core edges (columns < KC) of the half's rows in row
+// order, edge order within a row (a row's extension edge, its last, skipped).  Phase A reads the
+// stream's wrap-table offsets and LQ entries a fixed number of positions ahead, across rows.
+template <int BG>
+struct FrStream {
+    int start[64] = {};   // position of row i's edge 0 in its owner's stream
+    int n[2] = {};
+    int row[2][256] = {}, k[2][256] = {};
+    bool ok = true;
+    constexpr FrStream() {
+        using P = BGT<BG>;
+        for (int i = 0; i < P::MB; ++i) {
+            const int hh = kFrPlan<BG>.owner[i];
+            start[i] = n[hh];
+            for (int e = P::RS[i]; e < P::RS[i + 1]; ++e) {
+                if (P::COL[e] < P::KC) {
+                    ok = ok && n[hh] < 256 && e - P::RS[i] == n[hh] - start[i];   // core edges first
+                    if (n[hh] < 256) row[hh][n[hh]] = i, k[hh][n[hh]] = e - P::RS[i];
+                    ++n[hh];
+                } else {
+                    ok = ok && e == P::RS[i + 1] - 1 && i >= 4;   // the extension edge last
+                }
+            }
+        }
+    }
+};
+template <int BG>
+constexpr FrStream<BG> kFrStr{};
+static_assert(kFrStr<1>.ok && kFrStr<2>.ok, "frame core-edge stream");
+#ifndef LDPC5G_FR_DA
+#define LDPC5G_FR_DA 1   // stream positions the LQ reads run ahead
+#endif
+#ifndef LDPC5G_FR_DT
+#define LDPC5G_FR_DT 3   // stream positions the wrap-table reads run ahead
+#endif
+constexpr int kFrDA = LDPC5G_FR_DA, kFrDT = LDPC5G_FR_DT;
+static_assert(kFrDA >= 1 && kFrDT > kFrDA, "stream read distances");
+
 // V(i, k) mod Zc of edge k of row i; the same relative to the row's frame (thread s runs check node
 // s - off, so edge k's column entry is s + fr_cof); frame of LDS row i for half H's phase B
 template <int BG>

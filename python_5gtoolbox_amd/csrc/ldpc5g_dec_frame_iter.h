@@ -31,24 +31,38 @@
             constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
             if constexpr (p < kFrPlan<BG>.nx[hh]) xr[p % XP] = llrx(kFrPlan<BG>.xlist[hh][p]);
         };
-        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202); core-edge
-        // LQ reads one edge ahead, their wrap-table offsets two ahead
+        // ---- phase A: new row state from LQ_old (:117-123, _min_sum_process :186-202).  The
+        // half's core-edge stream (FrStream): entry p's wrap-table offset is read kFrDT positions
+        // ahead and its LQ kFrDA ahead, across row boundaries (slots p % kFrDT, p % kFrDA)
         struct RowSt {
             T mA, mB, min1, min2;
             uint32_t u, idxo, idx, negs;
             bool par;
-            T ab;
-            uint32_t tb[2];
         };
-        auto aloadt = [&](RowSt& r, auto ic, auto kc3) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k3 = decltype(kc3)::value;
-            if constexpr (k3 < d)
-                if constexpr (P::COL[e0 + k3] < KC) r.tb[k3 % 2] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k3) * 4u);
+        uint32_t tbs[kFrDT];
+        T abq[kFrDA];
+        auto sload_t = [&](auto hc, auto pc_) {
+            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
+            if constexpr (p < kFrStr<BG>.n[hh]) {
+                constexpr int i = kFrStr<BG>.row[hh][p], k = kFrStr<BG>.k[hh][p];
+                tbs[p % kFrDT] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k) * 4u);
+            }
         };
-        auto aload = [&](RowSt& r, auto ic, auto kc2) {
-            constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i), k2 = decltype(kc2)::value;
-            if constexpr (k2 < d)
-                if constexpr (P::COL[e0 + k2] < KC) r.ab = at((uint32_t)(P::COL[e0 + k2] * kFrColB) + r.tb[k2 % 2]);
+        auto sload_a = [&](auto hc, auto pc_) {
+            constexpr int hh = decltype(hc)::value, p = decltype(pc_)::value;
+            if constexpr (p < kFrStr<BG>.n[hh]) {
+                constexpr int i = kFrStr<BG>.row[hh][p], k = kFrStr<BG>.k[hh][p];
+                abq[p % kFrDA] = at((uint32_t)(P::COL[P::RS[i] + k] * kFrColB) + tbs[p % kFrDT]);
+            }
+        };
+        // core edge k of row i: its LQ entry, and the stream moved on by one
+        auto snext = [&](auto ic, auto kc) -> T {
+            constexpr int i = decltype(ic)::value, k = decltype(kc)::value;
+            constexpr int hh = kFrPlan<BG>.owner[i], p = kFrStr<BG>.start[i] + k;
+            const T a = abq[p % kFrDA];
+            sload_a(std::integral_constant<int, hh>{}, std::integral_constant<int, p + kFrDA>{});
+            sload_t(std::integral_constant<int, hh>{}, std::integral_constant<int, p + kFrDT>{});
+            return a;
         };
         auto rowA = [&](auto ic) {
             constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);
@@ -56,18 +70,13 @@
             get_state(ic, r.mA, r.mB, r.u, r.idxo);
             r.min1 = FT<T>::inf(), r.min2 = FT<T>::inf();
             r.idx = 0, r.negs = 0, r.par = false;
-            aloadt(r, ic, std::integral_constant<int, 0>{});
-            aloadt(r, ic, std::integral_constant<int, 1>{});
-            aload(r, ic, std::integral_constant<int, 0>{});
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
                 const T rold = xsign_v(pick(r.idxo == (uint32_t)k, r.mB, r.mA), r.u, mv);
                 asm("v_add_u32 %0, %1, %1" : "=v"(r.u) : "v"(r.u));   // u <<= 1, all-VGPR form
                 T a;
                 if constexpr (j < KC) {
-                    a = r.ab;
-                    aload(r, ic, std::integral_constant<int, k + 1>{});
-                    aloadt(r, ic, std::integral_constant<int, k + 2>{});
+                    a = snext(ic, kc);
                     __builtin_amdgcn_sched_barrier(0);
                     r.par ^= a < T(0);
                 } else {
@@ -111,7 +120,7 @@
             sfor<0, d>([&](auto kc) {
                 constexpr int k = decltype(kc)::value, j = P::COL[e0 + k];
                 if constexpr (j < KC) {
-                    const T a = at((uint32_t)(j * kFrColB) + rot(fr_cof<BG>(i, k)));
+                    const T a = snext(ic, kc);
                     par ^= a < T(0);
                     mn = fmin(mn, fabs(a));
                     sx ^= FT<T>::sbits(a);
@@ -126,7 +135,11 @@
             put_state(ic, T(0), alpha * x2, sx >> 31, (uint32_t)(d - 1));
         };
         if (active) {
-            per_half([&](auto hc) { sfor<0, XP>([&](auto pc_) { xload(hc, pc_); }); });
+            per_half([&](auto hc) {
+                sfor<0, XP>([&](auto pc_) { xload(hc, pc_); });
+                sfor<0, kFrDT>([&](auto pc_) { sload_t(hc, pc_); });
+                sfor<0, kFrDA>([&](auto pc_) { sload_a(hc, pc_); });
+            });
             sfor<0, MB>([&](auto ic) {   // one branch per row: bounded live ranges
                 constexpr int i = decltype(ic)::value;
                 if (h == kFrPlan<BG>.owner[i]) {

@@ -2,7 +2,11 @@
 each decoded alone through MixedBatch (layered OMS beta=0.5, L=8, rate-matched), event-timed, with
 its lane-op fraction on the algorithmic count, beside the whole mixed batch.
 
-    python tools/c4_groups_probe.py
+    python tools/c4_groups_probe.py [f64]
+
+f64: the reference-precision plan instead (float64 rows, float64 flooding OMS beta=0.5).
+Per group also the workgroups of its plan and their CU time (workgroups x time when they all fit
+on the GPU at once: a lower bound on what the group costs inside the mixed plan).
 """
 import os
 import sys
@@ -45,21 +49,36 @@ def main():
     llr = torch.zeros((len(cfgs), lay["max_E"]), dtype=torch.float32, device=dev)
     for t_, x in enumerate(llrs):
         llr[t_, :x.numel()] = x
-    dn = rrp(llr, torch.empty((lay["dn"],), dtype=torch.float32, device=dev))
+    f64 = "f64" in sys.argv[1:]
+    dt = torch.float64 if f64 else torch.float32
+    sched = "flooding" if f64 else "layered"
+    dn = rrp(llr, torch.empty((lay["dn"],), dtype=dt, device=dev))
     groups = [(bg, Zc, dn[r[2]:r[2] + r[1] * N].view(r[1], N)) for (bg, Zc, K, N, E), r in zip(meta, lay["rows"])]
-    tot = 0.0
+    tot = cu_tot = 0.0
     for (bg, Zc, K, N, E), grp in zip(meta, groups):
         mb = MixedBatch([grp])
-        ms = bench.ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, "layered", True), reps=10)
-        _, st, it = mb.decode(8, 1.0, 0.5, "layered", True)
+        ms = bench.ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, sched, True), reps=10)
+        _, st, it = mb.decode(8, 1.0, 0.5, sched, True)
+        nwg = _nwg(mb, sched)
         edges = int(it.sum().item()) * sum(bench._ROW_DEG[bg]) * Zc
         frac = edges * 13 / (ms * 1e-3) / 78.6e12
         tot += ms
+        cu_us = nwg * ms * 1e3 if nwg <= 256 else 256 * ms * 1e3
+        cu_tot += cu_us
         print(f"BG{bg} Zc={Zc:3d} E/N={E / N:.2f}: {ms * 1e3:7.1f} us  mean it {it.float().mean().item():.2f}  "
-              f"alg frac {frac:.3f}  ({n_per / ms * 1e3 / 1e6:.2f} M CB/s)", flush=True)
+              f"max it {int(it.max().item())}  alg frac {frac:.3f}  ({n_per / ms * 1e3 / 1e6:.2f} M CB/s)  "
+              f"{nwg} wg  {cu_us:8.0f} CU-us", flush=True)
     mb = MixedBatch(groups, flat=dn)
-    ms = bench.ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, "layered", True), reps=10)
-    print(f"sum of groups alone {tot * 1e3:.1f} us; all groups in one plan {ms * 1e3:.1f} us")
+    ms = bench.ev_ms(torch, lambda: mb.decode(8, 1.0, 0.5, sched, True), reps=10)
+    print(f"sum of groups alone {tot * 1e3:.1f} us; CU time {cu_tot:.0f} CU-us = {cu_tot / 256:.1f} us on 256 CUs; "
+          f"all groups in one plan {ms * 1e3:.1f} us")
+
+
+def _nwg(mb, sched):
+    """workgroups of the plan (its header: magic, schedule, nw1, nw2, ...)"""
+    host = mb._plans[sched][0]
+    hdr = host[:24].cpu().numpy().view(np.int32)
+    return int(hdr[2] + hdr[3])
 
 
 if __name__ == "__main__":

@@ -15,24 +15,24 @@ from concurrent.futures import ThreadPoolExecutor
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "python_5gtoolbox_amd", "csrc")
 HERE = os.path.dirname(os.path.abspath(__file__))
-FR = "ldpc5g_dec_frame.h"
+FRS = ("ldpc5g_dec_frame.h", "ldpc5g_dec_frame_iter.h")   # patched: the first file holding the text
 
 PATCHES = {
     # timing splits (wrong results)
-    "noB": [("        if constexpr (LDPC5G_FR_PIPE) {", "        if constexpr (false) {"),
-            ("                per_half([&](auto hc) {\n                    constexpr int H = decltype(hc)::value;\n"
-             "                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {\n"
-             "                        constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);\n"
-             "                        if constexpr (kFrPlan<BG>.lds[i]) {",
-             "                per_half([&](auto hc) {\n                    constexpr int H = decltype(hc)::value;\n"
-             "                    sfor<kFrPlan<BG>.gstart[g], kFrPlan<BG>.gstart[g + 1]>([&](auto ic) {\n"
-             "                        constexpr int i = decltype(ic)::value, e0 = P::RS[i], d = kFrPlan<BG>.deg(i);\n"
-             "                        if constexpr (false) {"),
-            ("                        } else if constexpr (kFrPlan<BG>.owner[i] == H) {\n                            T a, b;",
-             "                        } else if constexpr (false) {\n                            T a, b;")],
+    "noB": [("            if (active && !gdead) {", "            if (false) {")],
     "nobar": [("            lds_barrier();\n        });\n        }\n", "        });\n        }\n")],
     "plain": [("            else __hip_atomic_fetch_add(&acc, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);",
                "            else acc = r;")],
+    # phase A: the core edges' (LQ < 0) parity from f64 compares instead of the sign-word XOR
+    "noa": [("                    r.px ^= FT<T>::sbits(a);   // a core LQ is never -0.0 (frame_body's load)",
+             "                    r.par ^= a < T(0);")],
+    # phase-A latency splits (wrong results): no LDS reads of the core LQ / no ext LLR loads
+    "A_nolds": [("                if constexpr (P::COL[e0 + k2] < KC) r.ab = at((uint32_t)(P::COL[e0 + k2] * kFrColB) + r.tb[k2 % 2]);",
+                 "                if constexpr (P::COL[e0 + k2] < KC) r.ab = __builtin_bit_cast(T, ((uint64_t)r.tb[k2 % 2] << 32) | 0x3ff00000u);"),
+                ("                if constexpr (P::COL[e0 + k3] < KC) r.tb[k3 % 2] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k3) * 4u);",
+                 "                if constexpr (P::COL[e0 + k3] < KC) r.tb[k3 % 2] = tz + (uint32_t)fr_cof<BG>(i, k3) * 4u;")],
+    "A_noxl": [("            if constexpr (p < kFrPlan<BG>.nx[hh]) xr[p % XP] = llrx(kFrPlan<BG>.xlist[hh][p]);",
+                "            if constexpr (p < kFrPlan<BG>.nx[hh]) xr[p % XP] = T(1.5 + p) + T(sv);")],
     # DEAD kernel probe: the prologue's liveness loads kept, the plain iterations always
     "onlyplain": [("        if (live_x != all) {", "        if (live_x == 12345) {")],
 }
@@ -43,12 +43,13 @@ def make(spec):
     d = os.path.join(ROOT, "build", "frv", name)
     shutil.rmtree(d, ignore_errors=True)
     shutil.copytree(CSRC, d)
-    p = os.path.join(d, FR)
-    s = open(p).read()
+    texts = {f: open(os.path.join(d, f)).read() for f in FRS}
     for old, new in PATCHES.get(name.split("+")[0], []):
-        assert old in s, (name, old[:80])
-        s = s.replace(old, new)
-    open(p, "w").write(s)
+        hit = [f for f in FRS if old in texts[f]]
+        assert hit, (name, old[:80])
+        texts[hit[0]] = texts[hit[0]].replace(old, new)
+    for f in FRS:
+        open(os.path.join(d, f), "w").write(texts[f])
     out = os.path.join(ROOT, "build", "frdev", name + ".so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
