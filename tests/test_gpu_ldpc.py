@@ -275,6 +275,49 @@ def test_decode_frame_kernel_edge_cases(torch, dec, bg, pattern, rm):
             assert np.array_equal(g, r), (alpha, beta)
 
 
+@pytest.mark.parametrize("bg", [1, 2])
+def test_decode_frame_kernel_mixed_liveness(torch, dec, bg):
+    """One rate-matched (LDPC5G_RATE_MATCHED) float64 Zc = 384 launch whose codeblocks differ in
+    which extension rows are dead: the frame kernel finds each codeblock's live rows from its
+    prologue loads (wave ballots) and picks the dead-row or the plain iterations per workgroup, so
+    one launch runs both.  Codeblocks with 0 / 1 / 7 / 25 / all-but-one dead extension columns,
+    one dead column in the middle (a live row after a dead one), +0.0 vs -0.0 (-0.0 is not dead:
+    its bit pattern is not +0.0), filler-like huge LLRs, SNRs from -2 to 4 dB (codeblocks stop at
+    different iterations); NMS and OMS; vs the oracle's float64 decode_ldpc."""
+    rng = np.random.default_rng(77 + bg)
+    Zc, B = 384, 24
+    kb, mb = (22, 46) if bg == 1 else (10, 42)
+    ck = rng.integers(0, 2, (B, kb * Zc)).astype(np.int8)
+    dn = O.encode(ck, bg)
+    snr = rng.uniform(-2.0, 4.0, (B, 1))
+    llr = 2 * ((1 - 2 * dn) + rng.normal(size=dn.shape) * 10 ** (-snr / 20)) / 10 ** (-snr / 10)
+    nx = mb - 4
+    for b in range(B):
+        kind = b % 8
+        if kind == 1:
+            llr[b, -1 * Zc:] = 0.0
+        elif kind == 2:
+            llr[b, -7 * Zc:] = 0.0
+        elif kind == 3:
+            llr[b, -25 * Zc:] = 0.0
+        elif kind == 4:
+            llr[b, -(nx - 1) * Zc:] = 0.0
+        elif kind == 5:   # one dead column between live ones (ext row 4 + 10)
+            c0 = (kb + 2 + 10) * Zc - 2 * Zc
+            llr[b, c0:c0 + Zc] = 0.0
+        elif kind == 6:   # -0.0 everywhere in the tail: live (not +0.0)
+            llr[b, -7 * Zc:] = -0.0
+        elif kind == 7:   # a dead tail but one live entry in its last column
+            llr[b, -7 * Zc:] = 0.0
+            llr[b, -1] = 1.5
+    llr[::5, 3:kb * Zc:97] = 10 * np.abs(llr).max()   # filler-like entries (nr_ldpc_raterecover.py)
+    for alpha, beta in ((0.75, 0.0), (1.0, 0.5)):
+        got = dec.nr_decode_ldpc_batch(llr, Zc, bg, 8, "min-sum", alpha, beta, "flooding", rate_matched=True)
+        ref = O.decode_flooding(llr, Zc, bg, 8, alpha, beta, np.float64)
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r), (alpha, beta)
+
+
 @pytest.mark.parametrize("bg,Zc,B", [(1, 384, 1), (2, 384, 1), (1, 384, 7), (1, 64, 1), (1, 96, 2),
                                      (2, 72, 1), (2, 176, 3), (1, 208, 1), (2, 384, 8),
                                      # two chunks per wave (R = 2): more codeblocks than R = 1 fits
