@@ -99,6 +99,7 @@ struct CrcLds {
     uint32_t tab[2][256];
     uint32_t red[2][kCrcNT / 64];
     uint32_t part[2];
+    uint32_t dist[2];   // x^(bits after the chunk's last full word) mod g
 };
 __device__ __forceinline__ void crc_lds_init(CrcLds& S, int p0, int p1) {   // kCrcNT == 256
     S.tab[0][threadIdx.x] = kCrcTab.byte[p0][threadIdx.x];
@@ -190,6 +191,13 @@ __device__ void wg_crc_mem(const int8_t* src, int8_t* dst, int64_t nbits, int64_
     const int64_t q0 = chunk * kCrcChunkWords, q = q0 + threadIdx.x;
     const int64_t qf = min(q0 + kCrcChunkWords - 1, nfull - 1);   // last full word in the chunk
     const int al = ptr_align(src, dst);
+    // the chunk's distance to the message end (up to ~20 serial mulmods for a long message) is
+    // formed by the last thread before its loads, beside the other lanes' loads, instead of by
+    // thread 0 after the reduction; the barrier below publishes it
+    if (threadIdx.x == kCrcNT - 1)
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+            S.dist[i] = qf >= q0 ? crc_xpow(64 * (nfull - 1 - qf) + lw, p[i]) : 1u;
     uint32_t c[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) c[i] = 0;
@@ -219,8 +227,7 @@ __device__ void wg_crc_mem(const int8_t* src, int8_t* dst, int64_t nbits, int64_
         for (int i = 0; i < NP; ++i) {
             uint32_t r = 0;
             for (int w = 0; w < kCrcNT / 64; ++w) r ^= S.red[i][w];
-            if (qf >= q0 && r)
-                r = crc_mulmod(r, crc_xpow(64 * (nfull - 1 - qf) + lw, p[i]), kCrcPoly[p[i]].L, kCrcPoly[p[i]].g);
+            if (qf >= q0 && r) r = crc_mulmod(r, S.dist[i], kCrcPoly[p[i]].L, kCrcPoly[p[i]].g);
             if (lw > 0 && nfull >= q0 && nfull < q0 + kCrcChunkWords) r ^= S.part[i];
             out[i] = r;
         }
@@ -625,10 +632,15 @@ __global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restri
                                                           int64_t ldb, uint8_t* __restrict__ cb_ok,
                                                           uint32_t* tbrem) {
     __shared__ CrcLds S;
+    __shared__ uint32_t tb_dist;
     const RowGeo rg = row_geo(blockIdx.x, s0, gv, rm, ldc);
     const SchDev& s = rg.s;
     const int t = rg.t, c = rg.c;
     crc_lds_init(S, s.tbp, LDPC5G_CRC24B);
+    // the TB share's distance x^((C-1-c) cbz) mod g (up to ~20 serial mulmods): the last thread
+    // forms it while the others load the codeblock (its wave holds no word when cbz <= 12288 bits),
+    // not thread 0 after the pass; wg_crc_mem's closing barrier publishes it
+    if (threadIdx.x == kCrcNT - 1) tb_dist = crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp);
     const int8_t* row = ck + rg.dck_row;
     const int pp[2] = {s.tbp, LDPC5G_CRC24B};
     uint32_t v[2];
@@ -642,8 +654,7 @@ __global__ __launch_bounds__(kCrcNT) void tb_check_kernel(const int8_t* __restri
             cbr = crc_mulmod(v[1], crc_xpow(24, LDPC5G_CRC24B), 24, g) ^ crc_bits_msb(0u, tail, 24, 24, g);
         }
         cb_ok[rg.cbi] = cbr == 0u;
-        const uint32_t tbc = crc_mulmod(v[0], crc_xpow((int64_t)(s.C - 1 - c) * s.cbz, s.tbp), s.Ltb,
-                                        kCrcPoly[s.tbp].g);
+        const uint32_t tbc = crc_mulmod(v[0], tb_dist, s.Ltb, kCrcPoly[s.tbp].g);
         if (tbc) atomicXor(&tbrem[t], tbc);
     }
 }
