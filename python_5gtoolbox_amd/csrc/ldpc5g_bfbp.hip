@@ -185,6 +185,22 @@ constexpr bool bp_has_deg(int d) {
 // are f64 values in SGPR pairs made opaque at the start of each pass (otherwise the compiler hoists
 // every coefficient of both functions out of the iteration loop into VGPRs and spills them inside
 // the Horner chains).
+// LDPC5G_BP_FASTDIV: the two divisions with bounded operands (tanh's e / (e + 2), e + 2 in [2, 2.4e17],
+// and log's f / (2 + f), 2 + f in [1.4, 2.5]) by v_rcp_f64 + two Newton steps + one residual
+// correction (<= 1 ulp, not correctly rounded: inside §2's stated BP tolerance) instead of the
+// IEEE sequence (div_scale x 2, rcp, 4 fma, mul, div_fmas, div_fixup); and 2 atanh(P / t) as
+// log1p(2|P| / (|t| - |P|)) — one division where y = P / t and u = 2|y| / (1 - |y|) took two
+#ifndef LDPC5G_BP_FASTDIV
+#define LDPC5G_BP_FASTDIV 1
+#endif
+__device__ __forceinline__ double bp_div_bounded(double a, double b) {
+    if constexpr (!LDPC5G_BP_FASTDIV) return a / b;
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+}
 __device__ __forceinline__ double sk(double c) {
     asm volatile("" : "+s"(c));
     return c;
@@ -215,7 +231,7 @@ __device__ __forceinline__ double bp_tanh_half(double q, const BpTanhK& K) {
     const double p = fma(r * r, h, r);   // expm1(r)
     const int ki = (int)k;
     const double e = __builtin_amdgcn_ldexp(p, ki) + (__builtin_amdgcn_ldexp(1.0, ki) - 1.0);   // expm1(x)
-    return copysign(e / (e + 2.0), q);
+    return copysign(bp_div_bounded(e, e + 2.0), q);
 }
 struct BpAtanhK {   // log1p(u) = log(w) + c: w = m 2^e, m in [sqrt 1/2, sqrt 2), s = f/(2+f)
     double c[10];   // 2/(2n+1), n = 1..10
@@ -226,10 +242,8 @@ struct BpAtanhK {   // log1p(u) = log(w) + c: w = m 2^e, m in [sqrt 1/2, sqrt 2)
         sqrt_half = sk(0.7071067811865476), ln2_hi = sk(0.6931471787393093), ln2_lo = sk(1.8206359985041462e-09);
     }
 };
-// 2 atanh(y) = log1p(2|y| / (1 - |y|)) with y's sign, |y| < 1
-__device__ __forceinline__ double bp_two_atanh(double y, const BpAtanhK& K) {
-    const double a = fabs(y);
-    const double u = (2.0 * a) / (1.0 - a);
+// log1p(u), u >= 0
+__device__ __forceinline__ double bp_log1p(double u, const BpAtanhK& K) {
     const double w = 1.0 + u;
     const double cw = (u - (w - 1.0)) * __builtin_amdgcn_rcp(w);   // rounding of 1 + u (tiny)
     double m = __builtin_amdgcn_frexp_mant(w);
@@ -238,15 +252,31 @@ __device__ __forceinline__ double bp_two_atanh(double y, const BpAtanhK& K) {
     m = lo ? 2.0 * m : m;
     ex = lo ? ex - 1 : ex;
     const double f = m - 1.0;
-    const double s = f / (2.0 + f);
+    const double s = bp_div_bounded(f, 2.0 + f);
     const double s2 = s * s;
     double h = K.c[9];
 #pragma unroll
     for (int n = 8; n >= 0; --n) h = fma(h, s2, K.c[n]);
     const double lf = fma(s * s2, h, 2.0 * s);   // log(m) = 2 atanh(s)
     const double de = (double)ex;
-    const double r = fma(de, K.ln2_hi, lf + fma(de, K.ln2_lo, cw));
-    return copysign(r, y);
+    return fma(de, K.ln2_hi, lf + fma(de, K.ln2_lo, cw));
+}
+// 2 atanh(y) = log1p(2|y| / (1 - |y|)) with y's sign, |y| < 1
+__device__ __forceinline__ double bp_two_atanh(double y, const BpAtanhK& K) {
+    const double a = fabs(y);
+    return copysign(bp_log1p((2.0 * a) / (1.0 - a), K), y);
+}
+// the message 2 atanh(P / t) of an edge (P: the row's tanh product, t: the edge's own), clipped to
+// +-2 * 19.07 where |P / t| >= 1 (:157-162)
+__device__ __forceinline__ double bp_msg(double P, double t, const BpAtanhK& K) {
+    if constexpr (!LDPC5G_BP_FASTDIV) {
+        const double tmp2 = P / t;
+        return tmp2 >= 1.0 ? kBpClip : (tmp2 <= -1.0 ? -kBpClip : bp_two_atanh(tmp2, K));
+    }
+    const double aP = fabs(P), at = fabs(t);
+    const uint32_t neg = (uint32_t)(__double2hiint(P) ^ __double2hiint(t)) & 0x80000000u;
+    const double mag = aP >= at ? kBpClip : bp_log1p((2.0 * aP) / (at - aP), K);
+    return __hiloint2double(__double2hiint(mag) ^ (int)neg, __double2loint(mag));
 }
 
 // Consecutive base rows with disjoint core columns (the grouping of ldpc5g_dec_body.h RowGroups):
@@ -461,8 +491,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                             double r = 0.0;
                             if (k < d) {
                                 if (nzt == 0) {
-                                    const double tmp2 = prodt / tq[kk];
-                                    r = tmp2 >= 1.0 ? kBpClip : (tmp2 <= -1.0 ? -kBpClip : bp_two_atanh(tmp2, AK));
+                                    r = bp_msg(prodt, tq[kk], AK);
                                 } else if (nzt == 1 && k == zkt) {
                                     r = pnzt;   // prod(t[0:zk]) * prod(t[zk+1:]) (:166-172)
                                 }
