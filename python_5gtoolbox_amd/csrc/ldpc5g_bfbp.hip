@@ -368,6 +368,21 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
     const double* lrow = llr + (int64_t)(valid ? cb : 0) * ldl;
     int8_t* crow = ck + (int64_t)(valid ? cb : 0) * ldc;
     double* mrow = msg + (int64_t)(valid ? cb : 0) * NPAIR * Zc * 2;   // [P][z][2]
+    // The message accesses of the row loop: this workgroup's scratch from a uniform base (SGPRs,
+    // opaque per row like the z index) plus 32-bit per-lane byte offsets, so each load / store is
+    // one saddr access with one VALU add, not a 64-bit VALU address (sign extension + lshl_add_u64)
+    const double* msg_wg = msg + (int64_t)blockIdx.x * G * NPAIR * Zc * 2;
+    const uint32_t mlaneB = (uint32_t)((cl * NPAIR * Zc * 2 + par_lane) * 8);
+    auto opaque_s = [&]() {
+        uint64_t v = (uint64_t)(uintptr_t)msg_wg;
+        asm volatile("" : "+s"(v));
+        return (__attribute__((address_space(1))) unsigned char*)(uintptr_t)v;
+    };
+    // pair slot q, entry zo of this lane's codeblock
+    auto msg_at = [&](__attribute__((address_space(1))) unsigned char* mb, int q, int zo)
+        -> __attribute__((address_space(1))) double& {
+        return *(__attribute__((address_space(1))) double*)(mb + (mlaneB + (uint32_t)(q * Zc + zo) * 16u));
+    };
     // z / base pointers opaque per row or pass: otherwise LICM hoists the loop-invariant per-edge
     // addresses out of the iteration loop into registers (hundreds of scratch spills)
     auto opaque_z = [&]() {
@@ -398,12 +413,12 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
 
     double pf[KK];   // r_old of the next row's own edges, loaded ahead
     double pxl = 0.0;   // and the next row's extension-column LLR (rows >= 4)
-    auto load_row = [&](int i, int zo, __attribute__((address_space(1))) double* mr,
+    auto load_row = [&](int i, int zo, __attribute__((address_space(1))) unsigned char* mb,
                         const __attribute__((address_space(1))) double* lr) {
         const int d = bp_pairs_d<BG>().rs[i + 1] - bp_pairs_d<BG>().rs[i], q0 = bp_pairs_d<BG>().ps[i];
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
-            if (2 * kk < d) pf[kk] = mr[((q0 + kk) * Zc + zo) * 2 + par_lane];
+            if (2 * kk < d) pf[kk] = msg_at(mb, q0 + kk, zo);
         if (i >= 4) pxl = lr[(KB + i - pc) * Zc + zo];
     };
     int it = 0;
@@ -411,7 +426,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
         bool fail = false;
         uint64_t hdx = 0;   // ext decisions (LQ_old < 0) of the rows whose ext edge is this lane's
         if (active) {
-            load_row(0, opaque_z(), opaque_p(mrow), opaque_p(lrow));
+            load_row(0, opaque_z(), opaque_s(), opaque_p(lrow));
             for (int i = 0; i < MB; ++i) {
                 // next row group: the LDS sums ordered.  An LDS-only barrier: __syncthreads() would
                 // also wait (vmcnt(0)) for the next row's message loads and this row's stores
@@ -419,14 +434,14 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                 const int e0 = bp_pairs_d<BG>().rs[i], d = bp_pairs_d<BG>().rs[i + 1] - e0;
                 const int q0 = bp_pairs_d<BG>().ps[i];
                 const int zo = opaque_z();
-                const auto mr = opaque_p(mrow);
+                const auto mb = opaque_s();
                 const auto lr = opaque_p(lrow);
                 auto rotz = [&](int sft) { int m = zo + sft; return cl * Zc + (m >= Zc ? m - Zc : m); };
                 double tq[KK];
 #pragma unroll
                 for (int kk = 0; kk < KK; ++kk) tq[kk] = pf[kk];   // r_old
                 const double xl = pxl;
-                if (i + 1 < MB) load_row(i + 1, zo, mr, lr);
+                if (i + 1 < MB) load_row(i + 1, zo, mb, lr);
                 bool par = false;
                 int nz = 0, zk = 255;
                 double prod = 1.0, pnz = 1.0;   // product of all own t / of those with q != 0
@@ -500,7 +515,7 @@ __global__ __launch_bounds__(kBpThreads) void ldpc_bp_kernel(
                                 if (jcol[kk] >= 0)
                                     __hip_atomic_fetch_add(&acc[jcol[kk]], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             }
-                            mr[((q0 + kk) * Zc + zo) * 2 + par_lane] = r;
+                            msg_at(mb, q0 + kk, zo) = r;
                         }
                         bp_sched_point(kk);
                     }
