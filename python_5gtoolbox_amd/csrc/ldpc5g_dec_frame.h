@@ -304,6 +304,13 @@ __device__ __forceinline__ void frame_body(
         lrow = llr + (int64_t)out * ldl, crow = ck + (int64_t)out * ldc;
     }
     const T* lrow_x = lrow + (KB - pc) * Z;   // extension column of row i (>= 4): lrow_x[i * Zc + z]
+    // LLR e of a row base: the bases are workgroup-uniform (SGPRs), so with a 32-bit byte offset
+    // each load is one saddr access — a signed element index made it a 64-bit VALU address
+    auto ldg = [&](const T* base, int e) -> T {
+        using gT = const __attribute__((address_space(1))) T;
+        using gB = const __attribute__((address_space(1))) unsigned char;
+        return *(gT*)((gB*)(uintptr_t)base + (uint32_t)e * (uint32_t)sizeof(T));
+    };
     // own column jj of half h: column h, then columns 2..KH (half 0) / KH+1..KC-1 (half 1)
     auto jcol = [&](int jj) -> int { return jj == 0 ? h : jj + 1 + h * (KH - 1); };
     int* flagA = (int*)(smem + kFrPlan<BG>.fl_b);
@@ -377,7 +384,7 @@ __device__ __forceinline__ void frame_body(
 #pragma unroll
         for (int jj = 0; jj < KH; ++jj) {
             const int j = jcol(jj);
-            v0[jj] = lrow[(j < pc ? 0 : j - pc) * Z + s];
+            v0[jj] = ldg(lrow, (j < pc ? 0 : j - pc) * Z + s);
         }
         uint32_t wm = 0;
         if constexpr (KDEAD) {
@@ -389,7 +396,7 @@ __device__ __forceinline__ void frame_body(
                     constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
                     constexpr int c = (Z - kFrPlan<BG>.off[i]) % Z;
                     const int x = c == 0 ? s : (int)min((uint32_t)(s + c), (uint32_t)(s + c - Z));
-                    xv[decltype(xc)::value] = lrow_x[i * Z + x];
+                    xv[decltype(xc)::value] = ldg(lrow_x, i * Z + x);
                 });
                 sfor<0, NX>([&](auto xc) {
                     constexpr int p = decltype(xc)::value;
@@ -475,7 +482,7 @@ __device__ __forceinline__ void frame_body(
                 T vx[XB];
                 sfor<x0, x1>([&](auto xc) {
                     constexpr int i = kFrPlan<BG>.xlist[hh][decltype(xc)::value];
-                    vx[decltype(xc)::value - x0] = lrow_x[i * Z + xposf(i)];
+                    vx[decltype(xc)::value - x0] = ldg(lrow_x, i * Z + xposf(i));
                 });
                 __builtin_amdgcn_sched_barrier(0);
                 sfor<x0, x1>([&](auto xc) {

@@ -20,7 +20,7 @@
             if (c == 0) return sv;
             return (int)min((uint32_t)(sv + c), (uint32_t)(sv + c - Z));
         };
-        auto llrx = [&](int i) -> T { return lrow_x[i * Z + xpos(i)]; };
+        auto llrx = [&](int i) -> T { return ldg(lrow_x, i * Z + xpos(i)); };
         bool fail = false;
         uint64_t hdx = 0;   // hard decisions of the owned extension columns (LQ_old)
 
@@ -180,7 +180,7 @@
 #pragma unroll
             for (int jj = 0; jj < KH; ++jj) {
                 const int j = jcol(jj);
-                lf[jj] = lrow[(j < pc ? 0 : j - pc) * Z + sv];
+                lf[jj] = ldg(lrow, (j < pc ? 0 : j - pc) * Z + sv);
             }
             // hand-offs: the other column's message of this half's rows with both columns
             per_half([&](auto hc) {
