@@ -141,6 +141,8 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
     std::vector<DecWork> work[2];
     std::vector<CbRef> refs;
     int nz1 = 0;
+    bool span_err = false;
+    constexpr int kMaxN = 68 * 384;   // the longest codeblock row
     // lifting sizes ascending: the dispatcher hands workgroups to CUs in list order, and the
     // longest-running ones come first — a small-Zc workgroup holds G = 768 / Zc codeblocks (64 at
     // Zc = 12) and runs until its slowest one stops, nearly always all L iterations, while a
@@ -160,12 +162,19 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
                     r.llr_off = desc[v[s + c]].llr_off, r.ck_off = desc[v[s + c]].ck_off, r.out = v[s + c], r.pad = 0;
                     refs.push_back(r);
                 }
+                // a work item's codeblocks by LLR offset: the first is the lowest, the base of the
+                // layered kernel's 32-bit lane offsets (ldpc5g_dec_body.h), whose span is checked
+                std::sort(refs.begin() + w.first, refs.end(),
+                          [](const CbRef& a, const CbRef& b) { return a.llr_off < b.llr_off; });
+                if ((refs.back().llr_off - refs[w.first].llr_off + (int64_t)kMaxN) * 8 >= ((int64_t)1 << 32))
+                    span_err = true;
                 work[g].push_back(w);
             };
             if (part) emit(0, (int)part);
             for (size_t s = part; s < v.size(); s += G) emit(s, G);
             if (g == 0 && Zc == 384) nz1 = (int)((v.size() - part) / G);
         }
+    if (span_err) return fail(LDPC5G_ESIZE, "a work item's codeblock LLR rows span >= 4 GiB (rows of one (bgn, Zc) too far apart)");
     const int64_t need = (int64_t)sizeof(MixedPlanHdr) + (int64_t)(work[0].size() + work[1].size()) * (int64_t)sizeof(DecWork) +
                          (int64_t)refs.size() * (int64_t)sizeof(CbRef);
     if (!out || cap < need) return need;

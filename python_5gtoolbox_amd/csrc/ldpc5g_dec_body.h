@@ -382,6 +382,20 @@ __device__ __forceinline__ void dec_body(
         }
     }
     const int cl = valid ? cbl : 0;
+    // The row loop's ext-LLR loads as saddr accesses: a workgroup-uniform base (SGPRs: the first
+    // codeblock of the workgroup, whose row has the lowest offset — ldpc5g_capi.hip build_plan sorts
+    // a work item's codeblocks) plus a 32-bit per-lane byte offset (< 4 GiB: checked by the
+    // launchers / the plan), instead of a per-lane 64-bit VALU address per load
+    const T* lbase;
+    uint32_t lofs = 0;
+    if (work) {
+        const int64_t off0 = cbs[work[blockIdx.x].first].llr_off;
+        lbase = llr + off0;
+        if (valid) lofs = (uint32_t)((lrow - lbase) * TS);
+    } else {
+        lbase = llr + (int64_t)blockIdx.x * G * ldl;
+        if (valid) lofs = (uint32_t)((int64_t)cl * ldl * TS);
+    }
     const int tzb = valid ? t * TS : 0;   // byte offset of this thread's own column entry
     const uint32_t GT = (uint32_t)(G * TS), ZGT = (uint32_t)(Zc * G * TS);
     const uint32_t tzbw = (uint32_t)tzb - ZGT;   // own entry one wrap back (negative -> huge)
@@ -696,7 +710,11 @@ __device__ __forceinline__ void dec_body(
             constexpr int r0 = kGroups<BG>.start[g] > 4 ? kGroups<BG>.start[g] : 4;
             sfor<r0, (kGroups<BG>.start[g + 1] > r0 ? kGroups<BG>.start[g + 1] : r0)>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                xlb[g & 1][i - r0] = lrow[(KB + i - pc) * Zc + zv];   // unconditional: see zg
+                // unconditional (see zg); row base uniform, lane part 32-bit: one saddr load
+                using gT = const __attribute__((address_space(1))) T;
+                using gB = const __attribute__((address_space(1))) unsigned char;
+                gB* rowb = (gB*)(uintptr_t)lbase + (uint32_t)((KB + i - pc) * Zc * TS);
+                xlb[g & 1][i - r0] = *(gT*)(rowb + (lofs + (uint32_t)zv * (uint32_t)TS));
             });
         };
         prefetch(std::integral_constant<int, 0>{});
@@ -915,6 +933,8 @@ int launch_dec_t(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, int 
     // small batches (the per-codeblock drop-ins): no more slots than codeblocks, so one BG2 Zc=8
     // codeblock runs as a single wave and its ~30 row-group barriers per iteration are cheap
     const int G = std::min(dec_G(Zc, LAYERED), B);
+    if ((int64_t)G * ldl * (int64_t)sizeof(T) >= ((int64_t)1 << 32))   // 32-bit lane offsets (dec_body)
+        return fail(LDPC5G_ESIZE, "ldl=%lld: a workgroup's %d LLR rows span >= 4 GiB", (long long)ldl, G);
     constexpr int ZL = 384;   // BG1's largest lifting size has its own kernel (zc_shift)
     if constexpr (BG == 1)
         if (Zc == ZL && G == dec_cs<LAYERED>() / ZL)
