@@ -258,6 +258,25 @@ __device__ __forceinline__ void flood_body(
         }
     }
     const int cl = valid ? cbl : 0;
+    // LLR loads as saddr accesses: a workgroup-uniform base (the work item's first codeblock, its
+    // lowest row: build_plan sorts them) plus a 32-bit per-lane byte offset (< 4 GiB: checked by
+    // launch_flood_cfg / the plan) — as the layered kernel (ldpc5g_dec_body.h)
+    const T* lbase;
+    uint32_t lofs = 0;
+    if (work) {
+        lbase = llr + cbs[work[blockIdx.x].first].llr_off;
+        if (valid) lofs = (uint32_t)((lrow - lbase) * TS);
+    } else {
+        lbase = llr + (int64_t)blockIdx.x * G * ldl;
+        if (valid) lofs = (uint32_t)((int64_t)cl * ldl * TS);
+    }
+    // element e of column-major row position (uniform part `u`, this lane's entry `z`)
+    auto ldl_at = [&](int u, int zz) -> T {
+        using gT = const __attribute__((address_space(1))) T;
+        using gB = const __attribute__((address_space(1))) unsigned char;
+        gB* rowb = (gB*)(uintptr_t)lbase + (uint32_t)(u * TS);
+        return *(gT*)(rowb + (lofs + (uint32_t)zz * (uint32_t)TS));
+    };
     const int so = valid ? s : 0;
     const int tzb = so * TS;   // byte offset of this slot's own column entry
     const int zg = valid ? z : 0;   // loads issued without a branch stay in row 0 of CB 0
@@ -277,7 +296,7 @@ __device__ __forceinline__ void flood_body(
     using lds_u32 = __attribute__((address_space(3))) uint32_t;
     auto at = [&](int byte) -> lds_T& { return *(lds_T*)(uintptr_t)(uint32_t)byte; };
     auto own = [&](int j) -> lds_T& { return at(j * CS * TS + tzb); };
-    auto llrx = [&](int i) -> T { return lrow[(KB + i - pc) * Zc + zv]; };   // ext column of row i
+    auto llrx = [&](int i) -> T { return ldl_at((KB + i - pc) * Zc, zv); };   // ext column of row i
     auto per_half_init = [&](auto&& f) {
         sfor<0, NP>([&](auto pc_) {
             if (h == decltype(pc_)::value) f(pc_);
@@ -684,7 +703,7 @@ __device__ __forceinline__ void flood_body(
                 constexpr int jj = decltype(jc)::value;
                 const int j = h * KH + jj;
                 const int jl = min(j, KC - 1);   // unconditional: all loads in flight at once
-                lf[jj] = lrow[(jl < pc ? 0 : jl - pc) * Zc + zv];
+                lf[jj] = ldl_at((jl < pc ? 0 : jl - pc) * Zc, zv);
             });
         sfor<0, kGroups<BG>.n>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
@@ -867,6 +886,8 @@ int launch_flood_cfg(const T* llr, int8_t* ck, uint8_t* status, int32_t* iters, 
     const int H = ((G * Zc + 63) / 64) * 64;
     if (G < 1 || H > CS) return fail(LDPC5G_ESIZE, "flooding launch: %d codeblocks of Zc=%d per workgroup", G, Zc);
     if (ZCC > 0 && (Zc != ZCC || G != 1)) return fail(LDPC5G_ESIZE, "Zc=%d kernel launched for Zc=%d, G=%d", ZCC, Zc, G);
+    if ((int64_t)G * ldl * (int64_t)sizeof(T) >= ((int64_t)1 << 32))   // 32-bit lane offsets (flood_body)
+        return fail(LDPC5G_ESIZE, "ldl=%lld: a workgroup's %d LLR rows span >= 4 GiB", (long long)ldl, G);
     if (int rc = set_flood_lds<BG, T, NP, CS, DEAD, ZCC>(ofs)) return rc;
     const size_t lds = flood_lds_bytes<BG, T, NP, CS>();
     hipLaunchKernelGGL(kern, dim3((B + G - 1) / G), dim3(NP * H), lds, st, llr, ck, status, iters, B, Zc,
