@@ -29,6 +29,9 @@ PATCHES = {
     # phase A: rotated LQ offsets by VALU (rot: two adds + a min) instead of the wrap table
     "A_rot": [("                tbs[p % kFrDT] = *(lds_u32*)(uintptr_t)(tz + (uint32_t)fr_cof<BG>(i, k) * 4u);",
                "                tbs[p % kFrDT] = rot(fr_cof<BG>(i, k));")],
+    # phase A without the per-edge scheduling barrier
+    "nosb": [("                    a = snext(ic, kc);\n                    __builtin_amdgcn_sched_barrier(0);",
+              "                    a = snext(ic, kc);")],
     # phase-A latency splits (wrong results): no LDS reads of the core LQ / no ext LLR loads
     "A_nolds": [("                if constexpr (P::COL[e0 + k2] < KC) r.ab = at((uint32_t)(P::COL[e0 + k2] * kFrColB) + r.tb[k2 % 2]);",
                  "                if constexpr (P::COL[e0 + k2] < KC) r.ab = __builtin_bit_cast(T, ((uint64_t)r.tb[k2 % 2] << 32) | 0x3ff00000u);"),
