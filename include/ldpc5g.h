@@ -73,7 +73,9 @@ int ldpc5g_encode(const int8_t* ck, int8_t* dn, int32_t B, int32_t bgn, int32_t 
  *   iters  : [B] int32, check-node updates performed (flooding: the reference's loop index at
  *            its early return, else L; layered: iterations run)
  *   schedule LDPC5G_FLOODING works with F64 (bit-exact with the reference) and F32;
- *   LDPC5G_LAYERED requires F32. */
+ *   LDPC5G_LAYERED requires F32.
+ *   The codeblocks sharing a workgroup (up to 768 / Zc of them) are addressed with 32-bit byte
+ *   offsets: G * ldl * sizeof(element) >= 4 GiB returns LDPC5G_ESIZE (an ldl of 2^26 or more). */
 int ldpc5g_decode_ms(const void* llr, int32_t llr_dtype, int8_t* ck, uint8_t* status,
                      int32_t* iters, int32_t B, int32_t bgn, int32_t Zc, int32_t L,
                      double alpha, double beta, int32_t schedule, int32_t flags, int64_t ldl,
@@ -164,7 +166,10 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
  * when it is too small, so a first call with plan_bytes = 0 sizes it) or a negative error.  The
  * plan depends only on (desc, B, schedule).  Layout (opaque to callers): a 24-byte header, the
  * workgroups of each base graph by lifting size (BG1 Zc = 384 last, a partly filled workgroup
- * before the full ones), the codeblock references. */
+ * before the full ones), the codeblock references (sorted by llr_off within a workgroup: the
+ * kernels address a workgroup's rows from its lowest one with 32-bit offsets, so the rows of the
+ * codeblocks packed together — same (bgn, Zc), consecutive in desc order — must span < 4 GiB,
+ * else LDPC5G_ESIZE). */
 int64_t ldpc5g_mixed_plan(const ldpc5g_cb_desc_t* desc, int32_t B, int32_t schedule, void* plan,
                           int64_t plan_bytes);
 
