@@ -164,7 +164,7 @@ int ldpc5g_decode_ms_mixed(const ldpc5g_cb_desc_t* desc, int32_t B, const void* 
 /* Build the work list (plan) of a mixed batch into the caller's HOST buffer `plan` (pinned memory
  * recommended, `plan_bytes` long).  Returns the plan size in bytes (>= 0; the buffer is untouched
  * when it is too small, so a first call with plan_bytes = 0 sizes it) or a negative error.  The
- * plan depends only on (desc, B, schedule).  Layout (opaque to callers): a 24-byte header, the
+ * plan depends only on (desc, B, schedule).  Layout (opaque to callers): a 32-byte header, the
  * workgroups of each base graph by lifting size (BG1 Zc = 384 last, a partly filled workgroup
  * before the full ones), the codeblock references (sorted by llr_off within a workgroup: the
  * kernels address a workgroup's rows from its lowest one with 32-bit offsets, so the rows of the

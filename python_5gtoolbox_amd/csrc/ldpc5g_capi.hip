@@ -122,7 +122,10 @@ namespace {
 struct MixedPlanHdr {
     int32_t magic, schedule, nw1, nw2, nref;
     int32_t nz1;   // the last nz1 BG1 work items: Zc = 384 with a full G (the Zc = 384 kernels)
+    int32_t nz2;   // the same for BG2 (float64 flooding: the frame kernel)
+    int32_t pad;   // 32 bytes: the CbRef array after the work items stays 8-byte aligned
 };
+static_assert(sizeof(MixedPlanHdr) == 32 && sizeof(DecWork) % 8 == 0, "plan layout");
 constexpr int32_t kPlanMagic = 0x4c504d58;   // "XMPL"
 
 int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out, int64_t cap) {
@@ -140,7 +143,7 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
     }
     std::vector<DecWork> work[2];
     std::vector<CbRef> refs;
-    int nz1 = 0;
+    int nz1 = 0, nz2 = 0;
     bool span_err = false;
     constexpr int kMaxN = 68 * 384;   // the longest codeblock row
     // lifting sizes ascending: the dispatcher hands workgroups to CUs in list order, and the
@@ -172,14 +175,15 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
             };
             if (part) emit(0, (int)part);
             for (size_t s = part; s < v.size(); s += G) emit(s, G);
-            if (g == 0 && Zc == 384) nz1 = (int)((v.size() - part) / G);
+            if (Zc == 384) (g == 0 ? nz1 : nz2) = (int)((v.size() - part) / G);
         }
     if (span_err) return fail(LDPC5G_ESIZE, "a work item's codeblock LLR rows span >= 4 GiB (rows of one (bgn, Zc) too far apart)");
     const int64_t need = (int64_t)sizeof(MixedPlanHdr) + (int64_t)(work[0].size() + work[1].size()) * (int64_t)sizeof(DecWork) +
                          (int64_t)refs.size() * (int64_t)sizeof(CbRef);
     if (!out || cap < need) return need;
     unsigned char* p = (unsigned char*)out;
-    MixedPlanHdr h{kPlanMagic, schedule, (int32_t)work[0].size(), (int32_t)work[1].size(), (int32_t)refs.size(), nz1};
+    MixedPlanHdr h{kPlanMagic, schedule, (int32_t)work[0].size(), (int32_t)work[1].size(), (int32_t)refs.size(), nz1,
+                   nz2, 0};
     memcpy(p, &h, sizeof h);
     p += sizeof h;
     for (int g = 0; g < 2; ++g) {
@@ -231,8 +235,8 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
     const CbRef* r = (const CbRef*)(w2 + h.nw2);
     const bool lay = h.schedule == LDPC5G_LAYERED;
     // BG1's full Zc = 384 work items (the tail of its list) run the Zc = 384 kernels of mixed plans
-    // (layered float32, flooding float64; a mixed plan's float32 flooding items and BG2 items keep
-    // the generic kernels, although launch_flood_t has Zc = 384 kernels for those too) as their own
+    // (layered float32, flooding float64; a mixed plan's float32 flooding items keep the generic
+    // kernel, BG2's float64 ones go to the frame kernel below) as their own
     // launch on a third stream beside the rest (LDPC5G_MIX_Z3; in line on the caller's stream they
     // paid only when they fill the GPU on their own: config 4's 171 workgroups measured 1.04 ->
     // 1.17 ms split off in line)
@@ -246,9 +250,16 @@ int launch_plan(const MixedPlanHdr& h, const unsigned char* dev, const void* llr
         if (int rc = check_hip(hipEventRecord(side->fork, st), "hipEventRecord(fork)")) return rc;
         if (int rc = check_hip(hipStreamWaitEvent(side->s, side->fork, 0), "hipStreamWaitEvent(fork)")) return rc;
     }
+    // BG2's full Zc = 384 work items: the float64 frame kernel (ldpc5g_dec_frame.h), launched
+    // before BG2's other work items on the same stream
+    const int nzb = !lay && llr_dtype == LDPC5G_F64 ? std::min(h.nz2, h.nw2) : 0;
     for (int g = 0; g < 2; ++g) {
-        const int nwg = g == 0 ? h.nw1 - nz : h.nw2;
+        const int nwg = g == 0 ? h.nw1 - nz : h.nw2 - nzb;
         hipStream_t sg = g == 1 && side ? side->s : st;
+        if (g == 1 && nzb > 0)
+            if (int rc = launch_dec_mixed(2, llr_dtype, lay, llr_base, ck_base, status, iters, nzb,
+                                          w2 + (h.nw2 - nzb), r, L, alpha, beta, pc, dead, sg, true))
+                return rc;
         if (nwg > 0)
             if (int rc = launch_dec_mixed(g + 1, llr_dtype, lay, llr_base, ck_base, status, iters, nwg,
                                           g == 0 ? w1 : w2, r, L, alpha, beta, pc, dead, sg))

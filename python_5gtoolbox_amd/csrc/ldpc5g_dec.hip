@@ -49,8 +49,8 @@ int launch_dec_mixed(int bgn, int dtype, bool layered, const void* llr, int8_t* 
     if (dead) return launch_flood_mixed_dead(bgn, dtype, llr, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st, zc384);
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
-        if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
-            return launch_frame(1, false, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
+        if (zc384 && LDPC5G_FLOOD_FRAME)
+            return launch_frame(bgn, false, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
         if constexpr (!LDPC5G_FLOOD_FRAME)
             if (zc384 && bgn == 1)
                 return launch_flood_mixed_t<1, double, false, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);

@@ -24,8 +24,8 @@ int launch_flood_mixed_dead(int bgn, int dtype, const void* llr, int8_t* ck, uin
                             double alpha, double beta, int pc, hipStream_t st, bool zc384) {
     if (dtype == LDPC5G_F64) {
         const double* p = (const double*)llr;
-        if (zc384 && bgn == 1 && LDPC5G_FLOOD_FRAME)
-            return launch_frame(1, true, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
+        if (zc384 && LDPC5G_FLOOD_FRAME)
+            return launch_frame(bgn, true, p, ck, status, iters, nwg, 0, 0, L, alpha, beta, pc, work, cbs, st);
         if constexpr (!LDPC5G_FLOOD_FRAME)
             if (zc384 && bgn == 1)
                 return launch_flood_mixed_t<1, double, true, 384>(p, ck, status, iters, nwg, work, cbs, L, alpha, beta, pc, st);
