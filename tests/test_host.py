@@ -187,26 +187,47 @@ def test_product_fails_loudly_without_gpu():
 
 
 def test_mixed_plan_built_on_host():
-    """ldpc5g_mixed_plan is pure host code: sizing call, then the plan (header: schedule, BG1 / BG2
-    workgroups, codeblock refs) for 5 BG1 Zc=384 + 3 BG2 Zc=12 codeblocks, layered (G = 2 and
-    64 per workgroup) and flooding (G = 1 and 32)."""
+    """ldpc5g_mixed_plan is pure host code: sizing call, then the plan (32-byte header: schedule,
+    BG1 / BG2 workgroups, codeblock refs, the full Zc = 384 workgroups of each base graph) for 5
+    BG1 Zc=384 + 3 BG2 Zc=12 codeblocks, layered (G = 2 and 64 per workgroup) and flooding (G = 1
+    and 32); a work item's refs sorted by LLR offset (the kernels' 32-bit lane offsets start at its
+    first codeblock)."""
     lib = _lib.lib()
     d = (_lib.CbDesc * 8)()
     for k in range(8):
         d[k].bgn, d[k].Zc = (1, 384) if k < 5 else (2, 12)
-        d[k].llr_off, d[k].ck_off = 1000 * k, 2000 * k
+        d[k].llr_off, d[k].ck_off = 1000 * (7 - k), 2000 * k   # descending offsets
     for sched, nw1, nw2, nz1 in ((_lib.LAYERED, 3, 1, 2), (_lib.FLOODING, 5, 1, 5)):
         n = lib.ldpc5g_mixed_plan(d, 8, sched, None, 0)
-        assert n == 24 + 16 * (nw1 + nw2) + 24 * 8
+        assert n == 32 + 16 * (nw1 + nw2) + 24 * 8
         buf = (ctypes.c_ubyte * n)()
         assert lib.ldpc5g_mixed_plan(d, 8, sched, buf, n) == n
-        hdr = np.frombuffer(bytes(buf)[:24], np.int32)
+        hdr = np.frombuffer(bytes(buf)[:32], np.int32)
         assert hdr[1] == sched and hdr[2] == nw1 and hdr[3] == nw2 and hdr[4] == 8
         # the BG1 Zc=384 items: a partial workgroup first, then the nz1 full ones (the Zc = 384
-        # kernels' share, launched last)
-        assert hdr[5] == nz1
-        work = np.frombuffer(bytes(buf)[24:24 + 16 * nw1], np.int32).reshape(nw1, 4)
+        # kernels' share, launched last); no BG2 Zc=384 items here
+        assert hdr[5] == nz1 and hdr[6] == 0
+        work = np.frombuffer(bytes(buf)[32:32 + 16 * nw1], np.int32).reshape(nw1, 4)
         assert list(work[:, 2]) == ([1, 2, 2] if sched == _lib.LAYERED else [1] * 5)
+        refs = np.frombuffer(bytes(buf)[32 + 16 * (nw1 + nw2):], np.int64).reshape(8, 3)
+        works = np.frombuffer(bytes(buf)[32:32 + 16 * (nw1 + nw2)], np.int32).reshape(-1, 4)
+        for first, g in zip(works[:, 3], works[:, 2]):
+            offs = refs[first:first + g, 0]
+            assert list(offs) == sorted(offs)
+        assert sorted(refs[:, 2] & 0xffffffff) == list(range(8))   # every codeblock once (out index)
+    # BG2 Zc=384 codeblocks are counted for the frame kernel too
+    d2 = (_lib.CbDesc * 2)()
+    for k in range(2):
+        d2[k].bgn, d2[k].Zc, d2[k].llr_off, d2[k].ck_off = 2, 384, 20000 * k, 20000 * k
+    n = lib.ldpc5g_mixed_plan(d2, 2, _lib.FLOODING, None, 0)
+    buf = (ctypes.c_ubyte * n)()
+    assert lib.ldpc5g_mixed_plan(d2, 2, _lib.FLOODING, buf, n) == n
+    assert np.frombuffer(bytes(buf)[:32], np.int32)[6] == 2
+    # rows of one work item more than 4 GiB apart: refused
+    d2[1].bgn, d2[1].Zc = 1, 12
+    d2[0].bgn, d2[0].Zc = 1, 12
+    d2[1].llr_off = 1 << 30
+    assert lib.ldpc5g_mixed_plan(d2, 2, _lib.LAYERED, None, 0) == _lib.ESIZE
     d[3].Zc = 383
     assert lib.ldpc5g_mixed_plan(d, 8, _lib.LAYERED, None, 0) == _lib.EZC
     assert lib.ldpc5g_decode_ms_mixed_plan(None, None, None, 1, None, None, None, 8, 1.0, 0.0,
