@@ -186,11 +186,11 @@ int64_t build_plan(const ldpc5g_cb_desc_t* desc, int B, int schedule, void* out,
                    nz2, 0};
     memcpy(p, &h, sizeof h);
     p += sizeof h;
-    for (int g = 0; g < 2; ++g) {
-        memcpy(p, work[g].data(), work[g].size() * sizeof(DecWork));
+    for (int g = 0; g < 2; ++g) {   // (an empty vector's data() may be null: no memcpy from it)
+        if (!work[g].empty()) memcpy(p, work[g].data(), work[g].size() * sizeof(DecWork));
         p += work[g].size() * sizeof(DecWork);
     }
-    memcpy(p, refs.data(), refs.size() * sizeof(CbRef));
+    if (!refs.empty()) memcpy(p, refs.data(), refs.size() * sizeof(CbRef));
     return need;
 }
 
